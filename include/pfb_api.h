@@ -1,0 +1,190 @@
+/*
+ * pfb_api.h — C ABI of the MI355X-native oversampled polyphase filter bank (PFB).
+ *
+ * Drop-in boundary for the hot path of ska-telescope/ska-pst-dsp-model:
+ *   polyphase_analysis        (matlab/polyphase_analysis.m:1-129, Bunton PFB)
+ *   polyphase_analysis_padded (matlab/polyphase_analysis_padded.m:1-161, commutator PFB)
+ *   polyphase_synthesis       (matlab/polyphase_synthesis.m:1-325, golden inversion)
+ * and the stateful stream objects that call them
+ *   FilterBank.execute        (matlab/FilterBank.m:65-128)
+ *   InverseFilterBank.execute (matlab/InverseFilterBank.m:63-137)
+ * which the reference selects by name (FilterBank.m:36 str2func(analysis_function))
+ * or through the Python backend switch data_gen.channelize/synthesize
+ * (python/data_gen/channelize.py:19-92, synthesize.py:27-95).
+ *
+ * Everything crossing this boundary is plain C: integers, doubles, pointers, sizes.
+ * No C++ or torch types.  No exception crosses it: every entry point returns a
+ * pfb_status and pfb_last_error() returns the thread-local message (mirrors the
+ * reference's error(...) checks, e.g. InverseFilterBank.m:83-85).
+ *
+ * Data layout (complex float32, interleaved re/im = pfb_cf32):
+ *   single-channel time series : in[pol * pol_stride + t]
+ *   channelised data           : x[pol * pol_stride + t * n_chan + c]
+ *                                (per polarisation the Matlab memory order of an
+ *                                 (n_chan, n_dat) slice: channel fastest, then time)
+ * Buffers are device pointers (PFB_MEM_DEVICE, zero copy on the given stream) or host
+ * pointers (PFB_MEM_HOST, staged through the plan's device buffers; synchronous).
+ *
+ * Threading: a plan is bound to one device and is not thread safe (it carries the
+ * streaming state).  Different plans are independent; multi-GPU = one plan per GPU.
+ */
+#ifndef PFB_API_H
+#define PFB_API_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PFB_API_VERSION 1
+
+typedef struct pfb_cf32 {
+  float re;
+  float im;
+} pfb_cf32;
+
+typedef enum pfb_status {
+  PFB_OK = 0,
+  PFB_ERR_INVALID_ARG = 1,      /* e.g. N*de/nu, Ov*de/nu or Nf*de/nu not integral */
+  PFB_ERR_UNSUPPORTED = 2,      /* size combination with no compiled kernel */
+  PFB_ERR_HIP = 3,              /* HIP runtime error (message has hipGetErrorString) */
+  PFB_ERR_OOM = 4,
+  PFB_ERR_BUFFER_TOO_SMALL = 5, /* output capacity smaller than the required length */
+  PFB_ERR_NO_DEVICE = 6
+} pfb_status;
+
+typedef enum pfb_analysis_variant {
+  PFB_ANALYSIS_BUNTON = 0, /* polyphase_analysis.m */
+  PFB_ANALYSIS_PADDED = 1  /* polyphase_analysis_padded.m */
+} pfb_analysis_variant;
+
+typedef enum pfb_mem {
+  PFB_MEM_DEVICE = 0,
+  PFB_MEM_HOST = 1
+} pfb_mem;
+
+/* PFBWindow.m:10-16 lookup names, plus CUSTOM (explicit coefficients). */
+typedef enum pfb_window_kind {
+  PFB_WINDOW_NONE = 0,    /* no_window / identity_taper */
+  PFB_WINDOW_TUKEY = 1,   /* PFBWindow.m:30-44 */
+  PFB_WINDOW_TOP_HAT = 2, /* PFBWindow.m:63-68 */
+  PFB_WINDOW_HANN = 3,    /* PFBWindow.m:72-99 (temporal: applied per channel row) */
+  PFB_WINDOW_CUSTOM = 4   /* explicit coefficients (temporal: Nf values; spectral: L values) */
+} pfb_window_kind;
+
+/* ---------------------------------------------------------------- analysis */
+typedef struct pfb_analysis_desc {
+  int32_t variant;     /* pfb_analysis_variant */
+  int32_t n_chan;      /* "block" = N channels (polyphase_analysis.m:3) */
+  int32_t os_nu;       /* os_factor.nu */
+  int32_t os_de;       /* os_factor.de */
+  const double* taps;  /* prototype FIR taps (host memory, copied at create) */
+  int64_t n_taps;
+  int32_t n_pol;       /* polarisations processed per call */
+  int32_t device;      /* HIP device ordinal */
+} pfb_analysis_desc;
+
+typedef struct pfb_analysis_plan pfb_analysis_plan;
+
+/* Replaces: FilterBank constructor (FilterBank.m:26-63) + read_fir_filter_coeff. */
+pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* desc, pfb_analysis_plan** plan);
+pfb_status pfb_analysis_plan_destroy(pfb_analysis_plan* plan);
+
+/* Number of output samples per channel for n_dat input samples of a stateless call:
+ * Bunton K = floor((n_dat - P*N)/M) (polyphase_analysis.m:62), padded K = floor(n_dat/M)
+ * (polyphase_analysis_padded.m:75). */
+int64_t pfb_analysis_output_length(const pfb_analysis_plan* plan, int64_t n_dat);
+
+/* Stateless analysis — replaces polyphase_analysis(in, filt, block, os_factor) and
+ * polyphase_analysis_padded(...).  in: n_pol series of n_dat samples; out: n_pol x
+ * (K x n_chan).  *n_out receives K. */
+pfb_status pfb_analysis_execute(pfb_analysis_plan* plan, const pfb_cf32* in,
+                                int64_t in_pol_stride, int64_t n_dat, pfb_cf32* out,
+                                int64_t out_pol_stride, int64_t out_capacity,
+                                int64_t* n_out, int32_t mem, void* stream);
+
+/* Stateful stream — replaces FilterBank.execute (FilterBank.m:65-128): prepends the
+ * carried-over input, runs the analysis, trims the output to a multiple of nu and
+ * keeps input[T_out*M:] for the next call.  Input rounding hooks (rndInput etc.) are
+ * applied by the host mirror before this call. */
+pfb_status pfb_filterbank_execute(pfb_analysis_plan* plan, const pfb_cf32* in,
+                                  int64_t in_pol_stride, int64_t n_in, pfb_cf32* out,
+                                  int64_t out_pol_stride, int64_t out_capacity,
+                                  int64_t* n_out, int32_t mem, void* stream);
+int64_t pfb_filterbank_buffered(const pfb_analysis_plan* plan);
+pfb_status pfb_filterbank_reset(pfb_analysis_plan* plan);
+
+/* ---------------------------------------------------------------- synthesis */
+typedef struct pfb_synthesis_desc {
+  int32_t n_chan;             /* channels in the input */
+  int32_t os_nu;
+  int32_t os_de;
+  int32_t input_fft_length;   /* Nf */
+  int32_t input_overlap;      /* Ov */
+  int32_t spans_nyquist;      /* input_fully_spans_Nyquist_zone (1 = oversampled Low/Mid) */
+  int32_t combine;            /* coarse channels combined (polyphase_synthesis.m:198-239) */
+  int32_t apply_deripple;     /* deripple.apply_deripple */
+  const double* taps;         /* deripple.filter_coeff (host, copied) */
+  int64_t n_taps;
+  int32_t temporal_taper;     /* pfb_window_kind */
+  const double* temporal_coeffs; /* CUSTOM: Nf coefficients */
+  int32_t spectral_taper;     /* pfb_window_kind (NONE = identity_taper) */
+  const double* spectral_coeffs; /* CUSTOM: L = Nf*de/nu*n_chan coefficients */
+  int32_t n_pol;
+  int32_t device;
+} pfb_synthesis_desc;
+
+typedef struct pfb_synthesis_plan pfb_synthesis_plan;
+
+/* Replaces: InverseFilterBank constructor (InverseFilterBank.m:33-43) incl. the
+ * PFBWindow lookup and the freqz-based deripple response (polyphase_synthesis.m:138-150). */
+pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* desc, pfb_synthesis_plan** plan);
+pfb_status pfb_synthesis_plan_destroy(pfb_synthesis_plan* plan);
+
+/* n_blocks * output_keep for n_dat channelised samples (polyphase_synthesis.m:112-131). */
+int64_t pfb_synthesis_output_length(const pfb_synthesis_plan* plan, int64_t n_dat);
+
+/* Stateless synthesis — replaces polyphase_synthesis(in, spans, Nf, os, deripple,
+ * sample_offset, overlap, t_taper, s_taper, combine).  sample_offset is 1-based like
+ * Matlab (:99).  in: n_pol x (n_dat x n_chan); out: n_pol series. */
+pfb_status pfb_synthesis_execute(pfb_synthesis_plan* plan, const pfb_cf32* in,
+                                 int64_t in_pol_stride, int64_t n_dat, int64_t sample_offset,
+                                 pfb_cf32* out, int64_t out_pol_stride, int64_t out_capacity,
+                                 int64_t* n_out, int32_t mem, void* stream);
+
+/* Stateful stream — replaces InverseFilterBank.execute (InverseFilterBank.m:63-137):
+ * carry-over of n_dat - B*keep samples rounded up to a multiple of nu. */
+pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* plan, const pfb_cf32* in,
+                                          int64_t in_pol_stride, int64_t n_in, pfb_cf32* out,
+                                          int64_t out_pol_stride, int64_t out_capacity,
+                                          int64_t* n_out, int32_t mem, void* stream);
+int64_t pfb_inverse_filterbank_buffered(const pfb_synthesis_plan* plan);
+pfb_status pfb_inverse_filterbank_reset(pfb_synthesis_plan* plan);
+
+/* Blocks processed per channel-IFFT/block-kernel chunk (scratch = chunk * keep rows). */
+pfb_status pfb_synthesis_set_chunk_blocks(pfb_synthesis_plan* plan, int32_t blocks);
+
+/* ---------------------------------------------------------------- utilities */
+const char* pfb_last_error(void);
+int32_t pfb_api_version(void);
+int32_t pfb_device_count(void);
+/* Device memory helpers for callers without their own allocator (ctypes harness). */
+pfb_status pfb_device_malloc(int32_t device, int64_t bytes, void** ptr);
+pfb_status pfb_device_free(void* ptr);
+pfb_status pfb_memcpy_h2d(void* dst, const void* src, int64_t bytes, void* stream);
+pfb_status pfb_memcpy_d2h(void* dst, const void* src, int64_t bytes, void* stream);
+pfb_status pfb_stream_synchronize(void* stream);
+
+/* Kernel timing: average duration (ms) of the named kernel class over the launches
+ * recorded since the last reset, measured with HIP events on the plan's stream.
+ * which: 0 = analysis, 1 = synthesis channel-IFFT, 2 = synthesis block kernel. */
+pfb_status pfb_profile_enable(int32_t enable);
+pfb_status pfb_profile_read(int32_t which, double* total_ms, int64_t* launches, double* bytes);
+pfb_status pfb_profile_reset(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PFB_API_H */

@@ -1,0 +1,766 @@
+"""ORACLE — test infrastructure only.
+
+CPU restatement (NumPy, float64 by default) of the reference's oversampled-PFB hot
+path.  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module, and only as the *checker* (or as the
+timed CPU baseline).  The product path (``ska-pst-dsp-model_amd``) never imports it.
+
+Every function cites the Matlab lines it restates (paths relative to the reference
+repository ``ska-telescope/ska-pst-dsp-model``).
+
+Parity status — PARTIALLY PINNED.
+    The reference's golden model is Matlab (``polyphase_synthesis.m`` is declared the
+    golden inversion).  No MATLAB/Octave/MCR exists in the build image, the Python
+    implementation of the path lives in the un-vendored ``pfb`` package
+    (dean-shaff/pfb @ 130543e5, v0.7.0, absent), and the reference commits no golden
+    vectors.  This restatement is therefore pinned by
+      * the literal loop transliterations below (``*_literal``), which follow the
+        Matlab statements one by one and are cross-checked against the vectorised
+        forms;
+      * closed-form known answers derived from the cited lines (tone through the
+        analysis bank = N * H(...) * phase; unit round-trip gain);
+      * the reference's own fidelity tests: TestPureTone.m:55-89 (-60 dB),
+        TestImpulse.m:46-73 (-60 dB outside +-1 sample), TestFrequencyComb.m;
+      * the reference's real tap fixture config/PST_filtertaps.txt.
+    Bit-level parity against an actual Matlab run is UNPINNED.
+
+Precision placement follows the Matlab code: the analysis banks compute in the
+input class (single, ``polyphase_analysis.m:53``); the synthesis does its FFTs in
+double (``polyphase_synthesis.m:152-154``) and rounds ``FN`` (``:192``) and the
+output (``:131``) to the input class.  With ``round_like_matlab=False`` every stage
+stays float64 (the "exact" reference used for error budgets).
+"""
+from __future__ import annotations
+
+import math
+from fractions import Fraction
+from typing import Callable, Optional, Sequence
+
+import numpy as np
+
+__all__ = [
+    "Rational", "pad_filter", "polyphase_analysis", "polyphase_analysis_literal",
+    "polyphase_analysis_padded", "polyphase_analysis_padded_literal",
+    "polyphase_synthesis", "polyphase_synthesis_literal", "deripple_response",
+    "freqz_mag", "hann", "tukey_window", "top_hat_window", "no_window",
+    "hann_window", "pfb_window", "FilterBankOracle", "InverseFilterBankOracle",
+    "TwoStageFilterBankOracle", "TwoStageInverseFilterBankOracle",
+    "calc_output_nbins", "combine_permutation",
+]
+
+
+class Rational:
+    """``struct('nu', nu, 'de', de)`` of the reference (default_config.m:26-28)."""
+
+    def __init__(self, nu: int, de: int):
+        self.nu = int(nu)
+        self.de = int(de)
+
+    @classmethod
+    def from_str(cls, s: str) -> "Rational":
+        a, b = str(s).split("/")
+        return cls(int(a), int(b))
+
+    def normalize(self, n):  # normalize.m:17
+        return (self.de * n) / self.nu
+
+    def multiply(self, n):  # multiply.m:17
+        return (self.nu * n) / self.de
+
+    def __repr__(self):
+        return f"{self.nu}/{self.de}"
+
+
+def _os(os_factor) -> Rational:
+    if isinstance(os_factor, Rational):
+        return os_factor
+    if isinstance(os_factor, str):
+        return Rational.from_str(os_factor)
+    if isinstance(os_factor, dict):
+        return Rational(os_factor["nu"], os_factor["de"])
+    if isinstance(os_factor, (tuple, list)):
+        return Rational(*os_factor)
+    return Rational(os_factor.nu, os_factor.de)
+
+
+def _as_pnt(x) -> np.ndarray:
+    """Accept (n_pol, 1, n_dat), (n_pol, n_dat) or (n_dat,) and return (n_pol, n_dat)."""
+    x = np.asarray(x)
+    if x.ndim == 3:
+        assert x.shape[1] == 1, "analysis input must be (n_pol, 1, n_dat)"
+        return x[:, 0, :]
+    if x.ndim == 1:
+        return x[None, :]
+    return x
+
+
+def pad_filter(filt, n_chan: int) -> np.ndarray:
+    """pad_filter.m:10-12 — zero-pad the taps to ceil(len/n_chan)*n_chan."""
+    filt = np.asarray(filt).ravel()
+    phases = int(math.ceil(len(filt) / n_chan))
+    out = np.zeros(phases * n_chan, dtype=filt.dtype)
+    out[: len(filt)] = filt
+    return out
+
+
+# --------------------------------------------------------------------------- analysis
+def polyphase_analysis_literal(x, filt, block: int, os_factor) -> np.ndarray:
+    """Literal transliteration of polyphase_analysis.m:53-121 (small sizes only).
+
+    Loop per pol and per output sample k exactly as the Matlab code: multiply the
+    padded taps by the input block (:97), ``circshift(.., index)'`` (:102-105; the
+    apostrophe is the *conjugate* transpose), fold the P phases (:112-115) and
+    ``conj(ifft(temp2) * block^2)`` (:120).
+    """
+    os_ = _os(os_factor)
+    xin = _as_pnt(x).astype(np.complex128)
+    n_pol, n_dat = xin.shape
+    f = pad_filter(np.asarray(filt, dtype=np.float64), block)
+    step = (block * os_.de) // os_.nu
+    phases = len(f) // block
+    fl = len(f)
+    nblocks = (n_dat - fl) // step
+    out = np.zeros((n_pol, block, max(nblocks, 0)), dtype=np.complex128)
+    for p in range(n_pol):
+        in_pol = xin[p]
+        for k in range(nblocks):
+            in_block = in_pol[step * k: fl + step * k]
+            index = step * k - (step * k // block) * block
+            temp = np.conj(np.roll(f * in_block, index))
+            temp2 = np.zeros(block, dtype=np.complex128)
+            for m in range(phases):
+                temp2 = temp2 + temp[block * m: block * (m + 1)]
+            out[p, :, k] = np.conj(np.fft.ifft(temp2) * block ** 2)
+    return out
+
+
+def polyphase_analysis(x, filt, block: int, os_factor, dtype=np.complex128,
+                       round_like_matlab: bool = True) -> np.ndarray:
+    """Vectorised restatement of polyphase_analysis.m:53-121 (Bunton PFB).
+
+    out[p, c, k] = N * sum_n v_k[n] e^{-j 2 pi c n / N}, v_k[n] = u_k[(n - r_k) mod N],
+    u_k[n] = sum_m f[mN + n] x[Mk + mN + n], r_k = (M k) mod N,
+    K = floor((n_dat - P N) / M)  (:62).  Returns (n_pol, N, K).
+    """
+    os_ = _os(os_factor)
+    xin = _as_pnt(x)
+    rdt = np.float32 if dtype == np.complex64 else np.float64
+    xin = xin.astype(dtype)
+    n_pol, n_dat = xin.shape
+    N = int(block)
+    f = pad_filter(np.asarray(filt, dtype=np.float64), N).astype(rdt)
+    M = (N * os_.de) // os_.nu
+    P = len(f) // N
+    K = (n_dat - P * N) // M
+    if K <= 0:
+        return np.zeros((n_pol, N, 0), dtype=np.complex64 if round_like_matlab else dtype)
+    out = np.empty((n_pol, N, K), dtype=dtype)
+    k = np.arange(K)
+    r = (M * k) % N
+    n = np.arange(N)
+    gather = (n[None, :] - r[:, None]) % N  # v[n] = u[(n - r) mod N]
+    chunk = max(1, (1 << 22) // max(N, 1))
+    for p in range(n_pol):
+        xp = xin[p]
+        for k0 in range(0, K, chunk):
+            k1 = min(K, k0 + chunk)
+            u = np.zeros((k1 - k0, N), dtype=dtype)
+            for m in range(P):
+                base = M * k0 + m * N
+                view = np.lib.stride_tricks.as_strided(
+                    xp[base:], shape=(k1 - k0, N),
+                    strides=(M * xp.strides[0], xp.strides[0]), writeable=False)
+                u += f[m * N:(m + 1) * N][None, :] * view
+            v = np.take_along_axis(u, gather[k0:k1], axis=1)
+            out[p, :, k0:k1] = (N * np.fft.fft(v, axis=1)).T
+    if round_like_matlab:
+        out = out.astype(np.complex64)
+    return out
+
+
+def polyphase_analysis_padded_literal(x, filt, block: int, os_factor) -> np.ndarray:
+    """Literal transliteration of polyphase_analysis_padded.m:56-156 (small sizes).
+
+    Data mask with zero history (:101-102), ``sum(filt_2d .* mask_2d, 2)`` (:118),
+    shift-by-step + flipped new samples (:121-126), barrel-rotator circular shift
+    (:132-144), ``block^2 * ifft`` (:147) and the final circular shift by
+    -sample_delay_shift along time (:156).
+    """
+    os_ = _os(os_factor)
+    xin = _as_pnt(x).astype(np.complex128)
+    n_pol, n_dat = xin.shape
+    filt = np.asarray(filt, dtype=np.float64).ravel()
+    step = (block * os_.de) // os_.nu
+    overlap = block - step
+    nblocks = n_dat // step
+    sds = int(math.ceil((len(filt) - 1) / 2 / step))
+    fp = pad_filter(filt, block)
+    phases = len(fp) // block
+    f2d = fp.reshape(phases, block).T  # column-major reshape (block, phases)
+    out = np.zeros((n_pol, block, nblocks), dtype=np.complex128)
+    for p in range(n_pol):
+        in_pol = xin[p]
+        mask = np.zeros(block * phases, dtype=np.complex128)
+        mask2d = mask.reshape(phases, block).T
+        bri = 0
+        for idx in range(1, nblocks + 1):
+            ypfb = np.sum(f2d * mask2d, axis=1)
+            mask[step:] = mask[:-step].copy() if step < len(mask) else mask[step:]
+            # in_pol(idx*step:-1:(idx-1)*step+1) in 1-based Matlab indexing
+            mask[:step] = in_pol[(idx - 1) * step: idx * step][::-1]
+            mask2d = mask.reshape(phases, block).T
+            if bri == 0:
+                y1s = ypfb
+            else:
+                index = ((os_.nu - bri) * overlap) % block
+                y1s = np.roll(ypfb, -index)
+            out[p, :, idx - 1] = (block ** 2) * np.fft.ifft(y1s)
+            bri = (bri + 1) % os_.nu
+    out = np.roll(out, -sds, axis=2)
+    return out
+
+
+def polyphase_analysis_padded(x, filt, block: int, os_factor, dtype=np.complex128,
+                              round_like_matlab: bool = True) -> np.ndarray:
+    """Vectorised restatement of polyphase_analysis_padded.m:56-156 (commutator PFB).
+
+    y_q[n] = sum_p f[pN + n] x[qM - 1 - pN - n]  (x[<0] = 0; one-block delay),
+    index_q = 0 if q mod nu == 0 else ((nu - q mod nu)(N - M)) mod N,
+    z[n] = y[(n + index_q) mod N],  Y[c, q] = N sum_n z[n] e^{+j 2 pi c n / N},
+    out[:, :, t] = Y[:, :, (t + sds) mod K],  K = floor(n_dat / M), sds = ceil((Lh-1)/(2M)).
+    The maths is single precision in Matlab (taps cast, :56) but the output array is
+    double (:104); with round_like_matlab the values are rounded to float32 and kept
+    in a complex128 container like Matlab.
+    """
+    os_ = _os(os_factor)
+    xin = _as_pnt(x)
+    rdt = np.float32 if dtype == np.complex64 else np.float64
+    xin = xin.astype(dtype)
+    n_pol, n_dat = xin.shape
+    N = int(block)
+    filt = np.asarray(filt, dtype=np.float64).ravel()
+    f = pad_filter(filt, N).astype(rdt)
+    M = (N * os_.de) // os_.nu
+    P = len(f) // N
+    K = n_dat // M
+    sds = int(math.ceil((len(filt) - 1) / 2 / M))
+    out = np.empty((n_pol, N, K), dtype=dtype)
+    q = np.arange(K)
+    bri = q % os_.nu
+    index = np.where(bri == 0, 0, ((os_.nu - bri) * (N - M)) % N)
+    n = np.arange(N)
+    gather = (n[None, :] + index[:, None]) % N
+    PN = P * N
+    chunk = max(1, (1 << 22) // max(N, 1))
+    for p in range(n_pol):
+        # zero history of PN samples in front: xpad[PN + s] = x[s]
+        xpad = np.concatenate([np.zeros(PN, dtype=dtype), xin[p]])
+        for q0 in range(0, K, chunk):
+            q1 = min(K, q0 + chunk)
+            y = np.zeros((q1 - q0, N), dtype=dtype)
+            for m in range(P):
+                # x[qM - 1 - mN - n] -> xpad[PN + qM - 1 - mN - n]; descending in n
+                base = PN + q0 * M - 1 - m * N
+                # element (qq, n) at xpad[base + qq*M - n]
+                view = np.lib.stride_tricks.as_strided(
+                    xpad[base - (N - 1):], shape=(q1 - q0, N),
+                    strides=(M * xpad.strides[0], xpad.strides[0]), writeable=False)[:, ::-1]
+                y += f[m * N:(m + 1) * N][None, :] * view
+            z = np.take_along_axis(y, gather[q0:q1], axis=1)
+            out[p, :, q0:q1] = (N * N * np.fft.ifft(z, axis=1)).T
+    out = np.roll(out, -sds, axis=2)
+    if round_like_matlab:
+        out = out.astype(np.complex64).astype(np.complex128)
+    return out
+
+
+# --------------------------------------------------------------------------- windows
+def hann(L: int) -> np.ndarray:
+    """Matlab ``hann(L)`` (symmetric): 0.5 (1 - cos(2 pi n / (L - 1)))."""
+    if L == 1:
+        return np.ones(1)
+    n = np.arange(L)
+    return 0.5 * (1.0 - np.cos(2.0 * np.pi * n / (L - 1)))
+
+
+def no_window(in_dat, input_fft_length=None, input_discard=None):
+    """PFBWindow.m:22-27 (no_window) and identity_taper.m:1-2."""
+    return in_dat
+
+
+def tukey_window_coeffs(input_fft_length: int, input_discard: int) -> np.ndarray:
+    """PFBWindow.m:30-34 — ones with halves of hann(2*Ov) at both ends."""
+    w = np.ones(input_fft_length)
+    h = hann(2 * input_discard)
+    w[:input_discard] = h[:input_discard]
+    w[input_fft_length - input_discard:] = h[input_discard:]
+    return w
+
+
+def tukey_window(in_dat, input_fft_length, input_discard):
+    """PFBWindow.m:37-44 — multiply each channel row by the tukey window."""
+    return in_dat * tukey_window_coeffs(input_fft_length, input_discard)[None, :]
+
+
+def top_hat_window(in_dat, input_fft_length, input_discard):
+    """PFBWindow.m:63-68 — zero the first and last Ov samples of every row."""
+    out = np.array(in_dat, copy=True)
+    out[:, :input_discard] = 0
+    out[:, input_fft_length - input_discard:] = 0
+    return out
+
+
+def hann_window_coeffs(n_rows: int, input_fft_length: int) -> np.ndarray:
+    """PFBWindow.m:72-99 quirk: the window is applied along dim 1 (rows).
+
+    If the row count differs from input_fft_length the window is
+    circshift(hann(n_rows), n_rows/2); otherwise hann(input_fft_length) unshifted
+    (the ``fftshift(h,2)`` at :74 discards its result).
+    """
+    if n_rows != input_fft_length:
+        return np.roll(hann(n_rows), n_rows // 2)
+    return hann(input_fft_length)
+
+
+def hann_window(in_dat, input_fft_length, input_discard=None):
+    h = hann_window_coeffs(in_dat.shape[0], input_fft_length)
+    return h[:, None] * in_dat
+
+
+def pfb_window(name: str, input_fft_length: int, input_discard: int) -> Callable:
+    """PFBWindow.m:10-16 lookup: returns the taper handle for (Nf, Ov)."""
+    if name == "no_window":
+        return no_window
+    if name == "tukey":
+        return lambda a, nf=input_fft_length, ov=input_discard: tukey_window(
+            a, input_fft_length, input_discard)
+    if name == "top_hat":
+        return lambda a, nf=input_fft_length, ov=input_discard: top_hat_window(
+            a, input_fft_length, input_discard)
+    if name == "hann":
+        return lambda a, nf=input_fft_length, ov=input_discard: hann_window(
+            a, input_fft_length)
+    raise KeyError(f"PFBWindow: unknown window '{name}'")
+
+
+# --------------------------------------------------------------------------- synthesis
+def freqz_mag(h, n: int, count: int) -> np.ndarray:
+    """|H(e^{j pi k / n})| for k < count, H = DTFT of the taps (Matlab freqz(h,1,n)).
+
+    Exact via folding the taps modulo 2n and one FFT of length 2n.
+    """
+    h = np.asarray(h, dtype=np.float64).ravel()
+    L2 = 2 * n
+    folded = np.zeros(L2)
+    for s in range(0, len(h), L2):
+        seg = h[s:s + L2]
+        folded[:len(seg)] += seg
+    H = np.fft.fft(folded)
+    return np.abs(H[:count])
+
+
+def deripple_response(filt, n_chan: int, fn_width: int) -> np.ndarray:
+    """polyphase_synthesis.m:138-150 — 1/|H0| on passband_length+1 points,
+    H0 = freqz(filter_coeff, 1, n_chan * passband_length)."""
+    pl = fn_width // 2
+    return 1.0 / freqz_mag(filt, n_chan * pl, pl + 1)
+
+
+def combine_permutation(n_chan: int, combine: int) -> np.ndarray:
+    """polyphase_synthesis.m:198-239: slot ``chan`` reads input channel ``jchan``.
+
+    Returns jchan (0-based) for every chan (0-based)."""
+    jmap = np.arange(n_chan)
+    if combine <= 1:
+        return jmap
+    fcc = n_chan // combine
+    fco = n_chan
+    for chan in range(n_chan):
+        j = chan
+        output_channel = j // fco
+        if output_channel != 0:
+            raise ValueError(f"unexpected output channel={output_channel}")
+        fine = j - output_channel * fco
+        fine = (fine + fcc // 2) % fco
+        coarse = fine // fcc
+        fine = fine - coarse * fcc
+        coarse = (coarse + combine // 2) % combine
+        coarse = output_channel * combine + coarse
+        fine = (fine + fcc // 2) % fcc
+        jmap[chan] = coarse * fcc + fine
+    return jmap
+
+
+def _resolve_deripple(deripple):
+    if deripple is None:
+        return False, None
+    if isinstance(deripple, dict):
+        return bool(deripple.get("apply_deripple", 0)), deripple.get("filter_coeff")
+    if isinstance(deripple, (tuple, list)):
+        return bool(deripple[0]), deripple[1]
+    return bool(getattr(deripple, "apply_deripple")), getattr(deripple, "filter_coeff")
+
+
+def polyphase_synthesis_literal(x, input_fully_spans_nyquist, input_fft_length: int,
+                                os_factor, deripple=None, sample_offset: int = 1,
+                                input_overlap: Optional[int] = None,
+                                temporal_taper: Optional[Callable] = None,
+                                spectral_taper: Optional[Callable] = None,
+                                combine: int = 1) -> np.ndarray:
+    """Literal transliteration of polyphase_synthesis.m:60-316 (small sizes only).
+
+    Per block and pol: temporal taper (:179), transpose + Nf-point FFT (:184-185),
+    fftshift (:188), per-channel copy with the ``combine`` re-ordering (:193-240),
+    scalar deripple loop (:242-251), stitch (:253-278), spectral taper (:282),
+    ``ifft(FFFF)./(nu/de)`` (:285) and overlap-discard (:302).  ``sample_offset`` is
+    1-based like Matlab.  Returns (n_pol, 1, n_blocks * output_keep).
+    """
+    os_ = _os(os_factor)
+    x = np.asarray(x)
+    in_dtype = np.complex64 if x.dtype in (np.complex64, np.float32) else np.complex128
+    x = x[:, :, sample_offset - 1:]
+    n_pol, n_chan, n_dat = x.shape
+    Nf = int(input_fft_length)
+    Ov = Nf // 8 if input_overlap is None else int(input_overlap)
+    temporal_taper = temporal_taper or no_window
+    spectral_taper = spectral_taper or no_window
+    apply_deripple, filter_coeff = _resolve_deripple(deripple)
+    keep = Nf - 2 * Ov
+    n_blocks = (n_dat - 2 * Ov) // keep
+    L = Fraction(os_.de * Nf, os_.nu) * n_chan
+    Lov = Fraction(os_.de * Ov, os_.nu) * n_chan
+    assert L.denominator == 1 and Lov.denominator == 1
+    L, Lov = int(L), int(Lov)
+    Lkeep = L - 2 * Lov
+    out = np.zeros((n_pol, 1, max(n_blocks, 0) * Lkeep), dtype=in_dtype)
+    W = (Nf * os_.de) // os_.nu
+    W2 = W // 2
+    d2 = (Nf - W) // 2
+    if apply_deripple:
+        pl = W // 2
+        fr = deripple_response(filter_coeff, n_chan, W)  # 0-based fr[k], k=0..pl
+    jmap = combine_permutation(n_chan, combine)
+    for b in range(max(n_blocks, 0)):
+        for p in range(n_pol):
+            s = keep * b
+            in_dat = x[p, :, s:s + Nf].astype(np.complex128)
+            in_dat = temporal_taper(in_dat, Nf, Ov)
+            spectra = np.fft.fft(in_dat.T, Nf, axis=0)
+            spectra = np.fft.fftshift(spectra, axes=0)
+            FN = np.zeros((W, n_chan), dtype=in_dtype)
+            FFFF = np.zeros(n_chan * W, dtype=np.complex128)
+            for chan in range(n_chan):
+                FN[:, chan] = spectra[d2:d2 + W, jmap[chan]]
+                if apply_deripple:
+                    for ii in range(1, pl + 1):
+                        FN[ii - 1, chan] = FN[ii - 1, chan] * fr[pl - ii + 1]
+                        FN[pl + ii - 1, chan] = FN[pl + ii - 1, chan] * fr[ii - 1]
+                if not input_fully_spans_nyquist:
+                    FFFF[chan * W:(chan + 1) * W] = FN[:, chan]
+            if input_fully_spans_nyquist:
+                FFFF[:W2] = FN[W2:W, 0]
+                FFFF[n_chan * W - W2:] = FN[:W2, 0]
+                for chan in range(1, n_chan):
+                    i0 = (chan - 1) * W + W2
+                    FFFF[i0:i0 + W] = FN[:, chan]
+            FFFF = spectral_taper(FFFF[:, None], L, Ov)[:, 0]
+            iFFFF = np.fft.ifft(FFFF) / (os_.nu / os_.de)
+            out[p, 0, b * Lkeep:(b + 1) * Lkeep] = iFFFF[Lov:L - Lov]
+    return out
+
+
+def synthesis_tables(n_chan: int, Nf: int, os_factor, spans_nyquist: bool,
+                     deripple_gain: Optional[np.ndarray]):
+    """Per kept-bin tables of the re-ordered synthesis.
+
+    Position j' of the W-point inverse transform takes Nf-point FFT bin ``src[j']``,
+    real gain ``gain[j']`` and the four-step twiddle exponent ``expo[j']`` (the
+    twiddle is e^{+j 2 pi t0 expo / L}).  Spans-Nyquist folds the W/2 stitch shift
+    (polyphase_synthesis.m:265-278) into a signed-frequency exponent.
+    """
+    os_ = _os(os_factor)
+    W = (Nf * os_.de) // os_.nu
+    W2 = W // 2
+    d2 = (Nf - W) // 2
+    jp = np.arange(W)
+    if spans_nyquist:
+        j = (jp + W2) % W
+        expo = np.where(jp < W2, jp, jp - W)
+    else:
+        j = jp
+        expo = jp.copy()
+    src = (d2 + j + Nf // 2) % Nf
+    gain = np.ones(W)
+    if deripple_gain is not None:
+        g = np.asarray(deripple_gain)
+        gain = np.where(j < W2, g[np.clip(W2 - j, 0, W2)], g[np.clip(j - W2, 0, W2)])
+    return src, gain, expo
+
+
+def polyphase_synthesis(x, input_fully_spans_nyquist, input_fft_length: int, os_factor,
+                        deripple=None, sample_offset: int = 1,
+                        input_overlap: Optional[int] = None,
+                        temporal_taper=None, spectral_taper=None, combine: int = 1,
+                        round_like_matlab: bool = True, dtype=np.complex128) -> np.ndarray:
+    """Vectorised restatement of polyphase_synthesis.m:60-316 (golden inversion).
+
+    Batched over blocks: temporal taper, Nf-point FFT per channel, keep W bins
+    (fftshift + discard), deripple gain, stitch into the n_chan*W spectrum (spans
+    Nyquist: the DC channel's halves go to both ends), spectral taper, inverse FFT,
+    ÷(nu/de) and overlap-discard.  ``temporal_taper``/``spectral_taper`` are the
+    PFBWindow handles (callables); ``dtype`` complex64 makes a single-precision run
+    for the CPU baseline.
+    """
+    os_ = _os(os_factor)
+    x = np.asarray(x)
+    in_dtype = np.complex64 if x.dtype in (np.complex64, np.float32) else np.complex128
+    x = x[:, :, sample_offset - 1:]
+    n_pol, n_chan, n_dat = x.shape
+    Nf = int(input_fft_length)
+    Ov = Nf // 8 if input_overlap is None else int(input_overlap)
+    temporal_taper = temporal_taper or no_window
+    spectral_taper = spectral_taper or no_window
+    apply_deripple, filter_coeff = _resolve_deripple(deripple)
+    keep = Nf - 2 * Ov
+    n_blocks = max((n_dat - 2 * Ov) // keep, 0)
+    L = Fraction(os_.de * Nf, os_.nu) * n_chan
+    Lov = Fraction(os_.de * Ov, os_.nu) * n_chan
+    if L.denominator != 1 or Lov.denominator != 1:
+        raise ValueError("non-integral output_fft_length / output_overlap")
+    L, Lov = int(L), int(Lov)
+    Lkeep = L - 2 * Lov
+    W = (Nf * os_.de) // os_.nu
+    W2 = W // 2
+    d2 = (Nf - W) // 2
+    out_dtype = in_dtype if round_like_matlab else dtype
+    out = np.zeros((n_pol, 1, n_blocks * Lkeep), dtype=out_dtype)
+    if n_blocks == 0:
+        return out
+    jmap = combine_permutation(n_chan, combine)
+    gain = np.ones(W)
+    if apply_deripple:
+        fr = deripple_response(filter_coeff, n_chan, W)
+        j = np.arange(W)
+        gain = np.where(j < W2, fr[np.clip(W2 - j, 0, W2)], fr[np.clip(j - W2, 0, W2)])
+    cplx = dtype
+    bchunk = max(1, (1 << 23) // (n_chan * Nf))
+    for p in range(n_pol):
+        xp = np.ascontiguousarray(x[p])  # (n_chan, n_dat); combine re-ordering after the taper
+        for b0 in range(0, n_blocks, bchunk):
+            b1 = min(n_blocks, b0 + bchunk)
+            nb = b1 - b0
+            view = np.lib.stride_tricks.as_strided(
+                xp[:, keep * b0:], shape=(nb, n_chan, Nf),
+                strides=(keep * xp.strides[1], xp.strides[0], xp.strides[1]),
+                writeable=False).astype(cplx)
+            tap = np.stack([temporal_taper(view[i], Nf, Ov) for i in range(nb)])[:, jmap, :]
+            spec = np.fft.fftshift(np.fft.fft(tap, Nf, axis=2), axes=2)
+            FN = spec[:, :, d2:d2 + W]
+            if round_like_matlab:
+                FN = FN.astype(in_dtype).astype(cplx)
+            if apply_deripple:
+                FN = FN * gain[None, None, :]
+                if round_like_matlab:
+                    FN = FN.astype(in_dtype).astype(cplx)
+            G = FN.reshape(nb, n_chan * W)
+            if input_fully_spans_nyquist:
+                FFFF = np.roll(G, -W2, axis=1)
+            else:
+                FFFF = G
+            FFFF = np.stack([spectral_taper(FFFF[i][:, None], L, Ov)[:, 0] for i in range(nb)])
+            iF = np.fft.ifft(FFFF, axis=1) / (os_.nu / os_.de)
+            seg = iF[:, Lov:L - Lov].reshape(-1)
+            out[p, 0, b0 * Lkeep:b1 * Lkeep] = seg
+    return out
+
+
+def calc_output_nbins(nbins, channels, os_factor, filter_taps, input_fft_length,
+                      input_overlap):
+    """calc_output_nbins.m:17-27."""
+    os_ = _os(os_factor)
+    step = (channels * os_.de) // os_.nu
+    nblocks_pfb = (nbins - filter_taps) // step
+    output_pfb = (step * nblocks_pfb) // channels
+    input_keep = input_fft_length - 2 * input_overlap
+    nblocks_ipfb = (output_pfb - 2 * input_overlap) // input_keep
+    output_fft_length = os_.normalize(input_fft_length) * channels
+    output_overlap = os_.normalize(input_overlap) * channels
+    output_keep = output_fft_length - 2 * output_overlap
+    return int(output_keep * nblocks_ipfb)
+
+
+# --------------------------------------------------------------------------- streaming
+class FilterBankOracle:
+    """FilterBank.m:26-128 — analysis with input buffering and nu-trimming."""
+
+    def __init__(self, filt_coeff, n_chan, os_factor, analysis="polyphase_analysis",
+                 rndInput=False, rmsInput=0.0, rndOutput=False, rmsOutput=0.0):
+        self.filt_coeff = np.asarray(filt_coeff, dtype=np.float64).ravel()
+        self.n_chan = int(n_chan)
+        self.os_factor = _os(os_factor)
+        self.pfb_analysis = {"polyphase_analysis": polyphase_analysis,
+                             "polyphase_analysis_padded": polyphase_analysis_padded}[analysis]
+        self.rndInput, self.rmsInput = rndInput, rmsInput
+        self.rndOutput, self.rmsOutput = rndOutput, rmsOutput
+        self.input_buffer = None
+        self.buffered_samples = 0
+
+    def execute(self, x):
+        x = np.asarray(x)
+        if x.ndim == 2:
+            x = x[:, None, :]
+        if self.rndInput:  # :75-83
+            scale = 1.0
+            if self.rmsInput > 0:
+                scale = self.rmsInput / np.sqrt(np.var(x, ddof=1))
+            x = np.round(scale * x).astype(np.complex64)
+        if self.buffered_samples > 0:  # :85-88
+            x = np.concatenate([self.input_buffer, x], axis=2)
+            self.buffered_samples = 0
+        n_in = x.shape[2]
+        out = self.pfb_analysis(x, self.filt_coeff, self.n_chan, self.os_factor)
+        rem = out.shape[2] % self.os_factor.nu  # :93-104
+        if rem:
+            out = out[:, :, :out.shape[2] - rem]
+        if self.rndOutput:  # :106-113
+            scale = 1.0
+            if self.rmsOutput:
+                scale = self.rmsOutput / np.sqrt(np.var(out, ddof=1))
+            out = np.round(scale * out)
+        input_idat = Fraction(out.shape[2] * self.n_chan * self.os_factor.de, self.os_factor.nu)
+        self.buffered_samples = int(n_in - input_idat)  # :119-126
+        if self.buffered_samples > 0:
+            self.input_buffer = x[:, :, int(input_idat):]
+        return out
+
+
+class InverseFilterBankOracle:
+    """InverseFilterBank.m:25-137 — synthesis with buffering (deripple forced off
+    at :90 unless ``honour_deripple`` is set)."""
+
+    def __init__(self, filt_coeff, n_chan, os_factor, input_fft_length, input_overlap,
+                 temporal_taper="tukey", deripple=False, critical=False, combine=1,
+                 sample_offset=0, honour_deripple=False):
+        self.filt_coeff = np.asarray(filt_coeff, dtype=np.float64).ravel()
+        self.nchan = int(n_chan)
+        self.os_factor = _os(os_factor)
+        self.n_fft = int(input_fft_length)
+        self.overlap = int(input_overlap)
+        self.temporal_taper = pfb_window(temporal_taper, self.n_fft, self.overlap)
+        self.spectral_taper = no_window
+        self.deripple = deripple
+        self.honour_deripple = honour_deripple
+        self.critical = critical
+        self.combine = combine
+        self.sample_offset = sample_offset
+        self.input_buffer = None
+        self.buffered_samples = 0
+
+    def frequency_taper(self, name):  # :48-61
+        self.spectral_taper = pfb_window(name, self.n_fft, self.overlap)
+        return self
+
+    def execute(self, x):
+        x = np.asarray(x)
+        if self.buffered_samples > 0:
+            x = np.concatenate([self.input_buffer, x], axis=2)
+            self.buffered_samples = 0
+        n_pol, n_chan, n_dat = x.shape
+        spans = not self.critical
+        dr = bool(self.deripple) if self.honour_deripple else False
+        out = polyphase_synthesis(
+            x, spans, self.n_fft, self.os_factor,
+            {"apply_deripple": dr, "filter_coeff": self.filt_coeff},
+            self.sample_offset + 1, self.overlap, self.temporal_taper,
+            self.spectral_taper, self.combine)
+        modu = self.os_factor.nu
+        nu, de = self.os_factor.nu, self.os_factor.de
+        input_idat = Fraction(out.shape[2] * nu, n_chan * de)
+        buffered = n_dat - input_idat
+        rem = buffered % modu
+        if rem != 0:
+            buffered = buffered + modu - rem
+            input_idat = n_dat - buffered
+            output_ndat = input_idat * Fraction(n_chan * de, nu)
+            out = out[:, :, :int(math.floor(output_ndat))]
+        self.buffered_samples = int(buffered)
+        if self.buffered_samples > 0:
+            self.input_buffer = x[:, :, int(input_idat):]
+        return out
+
+
+class TwoStageFilterBankOracle:
+    """TwoStageFilterBank.m:58-116 — stage 2 over every stage-1 channel of pol 1."""
+
+    def __init__(self, stage1: FilterBankOracle, stage2_factory: Callable[[], FilterBankOracle],
+                 critical=False, single=False):
+        self.stage1 = stage1
+        self.stage2_factory = stage2_factory
+        self.stage2 = None
+        self.critical = critical
+        self.single = single
+
+    def execute(self, x):
+        out1 = self.stage1.execute(x)
+        nch1 = self.stage1.n_chan
+        if self.stage2 is None:
+            self.stage2 = [self.stage2_factory() for _ in range(nch1)]
+        os_ = self.stage1.os_factor
+        nch2_orig = self.stage2[0].n_chan
+        nch2 = nch2_orig * os_.de // os_.nu if self.critical else nch2_orig
+        offset = nch2_orig - nch2
+        if self.single:
+            nch1 = 1
+        out = None
+        for ich in range(nch1):
+            tmp = self.stage2[ich].execute(out1[0:1, ich:ich + 1, :])
+            if out is None:
+                out = np.zeros((1, nch1 * nch2, tmp.shape[2]), dtype=np.complex64)
+            base = ich * nch2
+            # Matlab 1-based (1:nch2/2) and (nch2/2:nch2): index nch2/2 is written twice
+            out[0, base:base + nch2 // 2, :] = tmp[0, :nch2 // 2, :]
+            out[0, base + nch2 // 2 - 1:base + nch2, :] = tmp[0, nch2 // 2 - 1 + offset:nch2 + offset, :]
+        return out
+
+
+class TwoStageInverseFilterBankOracle:
+    """TwoStageInverseFilterBank.m:75-157 — stage-2 inversion per coarse channel."""
+
+    def __init__(self, stage2_factory: Callable[[], InverseFilterBankOracle], nch2: int,
+                 combine: int = 1, single: bool = False):
+        self.stage2_factory = stage2_factory
+        self.nch2 = nch2
+        self.combine = combine
+        self.single = single
+        self.stage2 = None
+
+    def execute(self, x):
+        npol, nchan, _ = x.shape
+        nch_out = nchan // self.nch2
+        if self.stage2 is None:
+            self.stage2 = [self.stage2_factory() for _ in range(nch_out)]
+        os_ = self.stage2[0].os_factor
+        st_n = self.stage2[0].nchan
+        crit_n = st_n * os_.de // os_.nu
+        if self.nch2 == crit_n:
+            critical = True
+        elif self.nch2 == st_n:
+            critical = False
+            if self.combine > 1:
+                raise ValueError("cannot combine oversampled coarse channels")
+        else:
+            raise ValueError("invalid nchan")
+        nch_in = self.nch2 * self.combine
+        nch_out = nch_out // self.combine
+        if self.single:
+            nch_out = 1
+        out = None
+        for ich in range(nch_out):
+            st = self.stage2[ich]
+            st.critical = critical
+            st.combine = self.combine
+            tmp = st.execute(x[0:1, ich * nch_in:(ich + 1) * nch_in, :])
+            if out is None:
+                out = np.zeros((1, nch_out, tmp.shape[2]), dtype=np.complex128)
+            out[0, ich, :] = tmp[0, 0, :]
+        return out

@@ -1,0 +1,824 @@
+// pfb_api.hip — C ABI of the MI355X PFB engine (declared in include/pfb_api.h).
+//
+// Host-side plan management: tap padding, twiddle / deripple / window tables computed
+// in double and rounded once to float, device scratch, the FilterBank /
+// InverseFilterBank streaming state (carry-over buffers) and kernel dispatch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pfb_api.h"
+#include "pfb_kernels.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+pfb_status fail(pfb_status s, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return s;
+}
+
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(e_ == hipErrorOutOfMemory ? PFB_ERR_OOM : PFB_ERR_HIP, "%s: %s (%s:%d)", \
+                  #expr, hipGetErrorString(e_), __FILE__, __LINE__);                  \
+  } while (0)
+
+// ------------------------------------------------------------------ device buffer
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= bytes && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(n, 256));
+    if (e == hipSuccess) bytes = std::max<size_t>(n, 256);
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+template <class T>
+hipError_t upload(DevBuf& b, const std::vector<T>& v) {
+  hipError_t e = b.ensure(v.size() * sizeof(T));
+  if (e != hipSuccess) return e;
+  return hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+// e^{sign 2 pi i m / n}, accurate reduction in double
+std::vector<float2> twiddles(int64_t n, int sign) {
+  std::vector<float2> t((size_t)n);
+  for (int64_t m = 0; m < n; ++m) {
+    int64_t mm = m;
+    if (2 * mm > n) mm -= n;
+    const double a = 2.0 * M_PI * (double)mm / (double)n;
+    t[(size_t)m] = make_float2((float)std::cos(a), (float)(sign * std::sin(a)));
+  }
+  return t;
+}
+
+// ------------------------------------------------------------------ profiling
+struct ProfRec {
+  int which;
+  hipEvent_t a, b;
+  double bytes;
+};
+struct Profiler {
+  bool enabled = false;
+  std::vector<ProfRec> pending;
+  std::vector<hipEvent_t> pool;
+  double total_ms[3] = {0, 0, 0};
+  int64_t launches[3] = {0, 0, 0};
+  double bytes[3] = {0, 0, 0};
+  hipEvent_t get() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+  void drain() {
+    for (auto& r : pending) {
+      float ms = 0.f;
+      if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+        total_ms[r.which] += ms;
+        launches[r.which] += 1;
+        bytes[r.which] += r.bytes;
+      }
+      pool.push_back(r.a);
+      pool.push_back(r.b);
+    }
+    pending.clear();
+  }
+};
+Profiler g_prof;
+
+struct ProfScope {
+  hipEvent_t a = nullptr, b = nullptr;
+  int which;
+  double bytes;
+  hipStream_t s;
+  ProfScope(int w, double by, hipStream_t st) : which(w), bytes(by), s(st) {
+    if (g_prof.enabled) {
+      a = g_prof.get();
+      b = g_prof.get();
+      if (a) (void)hipEventRecord(a, s);
+    }
+  }
+  ~ProfScope() {
+    if (g_prof.enabled && a && b) {
+      (void)hipEventRecord(b, s);
+      g_prof.pending.push_back({which, a, b, bytes});
+    }
+  }
+};
+
+int64_t floordiv(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+}  // namespace
+
+// ====================================================================== analysis plan
+struct pfb_analysis_plan {
+  int device = 0;
+  int variant = 0, N = 0, nu = 1, de = 1, M = 0, P = 0, n_pol = 1, sds = 0;
+  int64_t n_taps = 0;
+  bool fused = false;
+  DevBuf taps, twN, scratch;
+  // streaming (FilterBank.m:13-14 input_buffer / buffered_samples)
+  DevBuf carry, work, stage_in, stage_out;
+  int64_t buffered = 0;
+};
+
+static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
+                               float2* out, int64_t out_ps, int64_t K, hipStream_t s) {
+  pfb::AnalysisArgs a{};
+  a.in = in;
+  a.in_pol_stride = in_ps;
+  a.n_dat = n_dat;
+  a.out = out;
+  a.out_pol_stride = out_ps;
+  a.K = K;
+  a.n_pol = p->n_pol;
+  a.N = p->N;
+  a.M = p->M;
+  a.P = p->P;
+  a.nu = p->nu;
+  a.sds = p->sds;
+  a.variant = p->variant;
+  a.taps = p->taps.as<float>();
+  a.twN = p->twN.as<float2>();
+  a.scratch = nullptr;
+  if (!p->fused) {
+    HIPCHK(p->scratch.ensure((size_t)p->n_pol * K * p->N * sizeof(float2)));
+    a.scratch = p->scratch.as<float2>();
+  }
+  const double bytes = (double)p->n_pol * (8.0 * n_dat + 8.0 * K * p->N);
+  ProfScope ps(0, bytes, s);
+  HIPCHK(pfb::launch_analysis(a, s));
+  return PFB_OK;
+}
+
+static int64_t analysis_K(const pfb_analysis_plan* p, int64_t n_dat) {
+  if (p->variant == pfb::kBunton) {
+    const int64_t k = floordiv(n_dat - (int64_t)p->P * p->N, p->M);
+    return std::max<int64_t>(k, 0);
+  }
+  return std::max<int64_t>(n_dat / p->M, 0);
+}
+
+extern "C" {
+
+const char* pfb_last_error(void) { return g_err.c_str(); }
+int32_t pfb_api_version(void) { return PFB_API_VERSION; }
+
+int32_t pfb_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_plan** out) {
+  if (!d || !out) return fail(PFB_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  if (d->variant != PFB_ANALYSIS_BUNTON && d->variant != PFB_ANALYSIS_PADDED)
+    return fail(PFB_ERR_INVALID_ARG, "unknown analysis variant %d", d->variant);
+  if (d->n_chan <= 0 || d->os_nu <= 0 || d->os_de <= 0 || d->os_de > d->os_nu)
+    return fail(PFB_ERR_INVALID_ARG, "invalid n_chan/os_factor (%d, %d/%d)", d->n_chan, d->os_nu,
+                d->os_de);
+  if (!d->taps || d->n_taps <= 0) return fail(PFB_ERR_INVALID_ARG, "no filter taps");
+  if (d->n_pol <= 0) return fail(PFB_ERR_INVALID_ARG, "n_pol must be positive");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(PFB_ERR_NO_DEVICE, "no HIP device available");
+  if (d->device < 0 || d->device >= ndev)
+    return fail(PFB_ERR_INVALID_ARG, "device %d out of range (%d devices)", d->device, ndev);
+  auto* p = new pfb_analysis_plan();
+  p->device = d->device;
+  p->variant = d->variant;
+  p->N = d->n_chan;
+  p->nu = d->os_nu;
+  p->de = d->os_de;
+  p->M = (int)(((int64_t)d->n_chan * d->os_de) / d->os_nu);  // floor, polyphase_analysis.m:56
+  p->n_taps = d->n_taps;
+  p->P = (int)((d->n_taps + d->n_chan - 1) / d->n_chan);    // pad_filter.m:10
+  p->n_pol = d->n_pol;
+  p->sds = (int)std::ceil((double)(d->n_taps - 1) / 2.0 / (double)p->M);  // padded.m:89
+  if (p->M <= 0) {
+    delete p;
+    return fail(PFB_ERR_INVALID_ARG, "commutator step M = floor(N de/nu) is zero");
+  }
+  if (!pfb::analysis_supported(p->N, p->P, p->variant, &p->fused)) {
+    delete p;
+    return fail(PFB_ERR_UNSUPPORTED, "no analysis kernel for n_chan=%d", d->n_chan);
+  }
+  if (hipSetDevice(p->device) != hipSuccess) {
+    delete p;
+    return fail(PFB_ERR_HIP, "hipSetDevice(%d) failed", d->device);
+  }
+  std::vector<float> taps((size_t)p->P * p->N, 0.f);
+  for (int64_t i = 0; i < d->n_taps; ++i) taps[(size_t)i] = (float)d->taps[i];  // cast(filt, 'single')
+  hipError_t e = upload(p->taps, taps);
+  if (e == hipSuccess) e = upload(p->twN, twiddles(p->N, -1));
+  if (e != hipSuccess) {
+    delete p;
+    return fail(PFB_ERR_HIP, "analysis plan upload: %s", hipGetErrorString(e));
+  }
+  *out = p;
+  return PFB_OK;
+}
+
+pfb_status pfb_analysis_plan_destroy(pfb_analysis_plan* p) {
+  if (!p) return PFB_OK;
+  (void)hipSetDevice(p->device);
+  p->taps.release();
+  p->twN.release();
+  p->scratch.release();
+  p->carry.release();
+  p->work.release();
+  p->stage_in.release();
+  p->stage_out.release();
+  delete p;
+  return PFB_OK;
+}
+
+int64_t pfb_analysis_output_length(const pfb_analysis_plan* p, int64_t n_dat) {
+  if (!p) return -1;
+  return analysis_K(p, n_dat);
+}
+
+pfb_status pfb_analysis_execute(pfb_analysis_plan* p, const pfb_cf32* in, int64_t in_ps,
+                                int64_t n_dat, pfb_cf32* out, int64_t out_ps, int64_t cap,
+                                int64_t* n_out, int32_t mem, void* stream) {
+  if (!p || (!in && n_dat > 0)) return fail(PFB_ERR_INVALID_ARG, "null argument");
+  if (n_dat < 0) return fail(PFB_ERR_INVALID_ARG, "negative n_dat");
+  HIPCHK(hipSetDevice(p->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t K = analysis_K(p, n_dat);
+  if (n_out) *n_out = K;
+  if (K == 0) return PFB_OK;
+  if (!out) return fail(PFB_ERR_INVALID_ARG, "null output");
+  if (cap < K) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld rows",
+                           (long long)cap, (long long)K);
+  if (mem == PFB_MEM_DEVICE) {
+    if (in_ps < n_dat || out_ps < K * p->N)
+      return fail(PFB_ERR_INVALID_ARG, "polarisation stride smaller than the data");
+    return analysis_run(p, (const float2*)in, in_ps, n_dat, (float2*)out, out_ps, K, s);
+  }
+  // host staging (synchronous)
+  HIPCHK(p->stage_in.ensure((size_t)p->n_pol * n_dat * sizeof(float2)));
+  HIPCHK(p->stage_out.ensure((size_t)p->n_pol * K * p->N * sizeof(float2)));
+  for (int q = 0; q < p->n_pol; ++q)
+    HIPCHK(hipMemcpyAsync(p->stage_in.as<float2>() + (size_t)q * n_dat, in + q * in_ps,
+                          n_dat * sizeof(float2), hipMemcpyHostToDevice, s));
+  pfb_status st = analysis_run(p, p->stage_in.as<float2>(), n_dat, n_dat,
+                               p->stage_out.as<float2>(), K * p->N, K, s);
+  if (st != PFB_OK) return st;
+  for (int q = 0; q < p->n_pol; ++q)
+    HIPCHK(hipMemcpyAsync(out + q * out_ps, p->stage_out.as<float2>() + (size_t)q * K * p->N,
+                          K * p->N * sizeof(float2), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return PFB_OK;
+}
+
+pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int64_t in_ps,
+                                  int64_t n_in, pfb_cf32* out, int64_t out_ps, int64_t cap,
+                                  int64_t* n_out, int32_t mem, void* stream) {
+  if (!p || (!in && n_in > 0)) return fail(PFB_ERR_INVALID_ARG, "null argument");
+  HIPCHK(hipSetDevice(p->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t total = p->buffered + n_in;
+  const hipMemcpyKind kin = mem == PFB_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  // input = cat(3, input_buffer, input)   (FilterBank.m:85-88)
+  HIPCHK(p->work.ensure((size_t)p->n_pol * std::max<int64_t>(total, 1) * sizeof(float2)));
+  float2* w = p->work.as<float2>();
+  for (int q = 0; q < p->n_pol; ++q) {
+    if (p->buffered > 0)
+      HIPCHK(hipMemcpyAsync(w + (size_t)q * total, p->carry.as<float2>() + (size_t)q * p->buffered,
+                            p->buffered * sizeof(float2), hipMemcpyDeviceToDevice, s));
+    if (n_in > 0)
+      HIPCHK(hipMemcpyAsync(w + (size_t)q * total + p->buffered, in + q * in_ps,
+                            n_in * sizeof(float2), kin, s));
+  }
+  const int64_t K = analysis_K(p, total);
+  const int64_t Kt = K - (K % p->nu);  // trim to a multiple of nu (FilterBank.m:93-104)
+  if (n_out) *n_out = Kt;
+  if (Kt > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld rows",
+                            (long long)cap, (long long)Kt);
+  if (Kt > 0) {
+    float2* dst;
+    int64_t dps;
+    if (mem == PFB_MEM_HOST) {
+      HIPCHK(p->stage_out.ensure((size_t)p->n_pol * K * p->N * sizeof(float2)));
+      dst = p->stage_out.as<float2>();
+      dps = K * p->N;
+    } else {
+      dst = (float2*)out;
+      dps = out_ps;
+      if (Kt != K) {  // kernels write K rows; stage when the caller sized for Kt only
+        HIPCHK(p->stage_out.ensure((size_t)p->n_pol * K * p->N * sizeof(float2)));
+        dst = p->stage_out.as<float2>();
+        dps = K * p->N;
+      }
+    }
+    pfb_status st = analysis_run(p, w, total, total, dst, dps, K, s);
+    if (st != PFB_OK) return st;
+    if (dst != (float2*)out) {
+      const hipMemcpyKind ko = mem == PFB_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+      for (int q = 0; q < p->n_pol; ++q)
+        HIPCHK(hipMemcpyAsync(out + q * out_ps, dst + (size_t)q * dps, Kt * p->N * sizeof(float2),
+                              ko, s));
+    }
+  }
+  // carry = input(:,:,input_idat+1:end), input_idat = T_out N de / nu   (FilterBank.m:119-126)
+  const int64_t input_idat = (Kt * p->N * p->de) / p->nu;
+  const int64_t nb = total - input_idat;
+  if (nb > 0) {
+    HIPCHK(p->carry.ensure((size_t)p->n_pol * nb * sizeof(float2)));
+    // carry may alias nothing in `work` (separate buffer); copy per pol
+    for (int q = 0; q < p->n_pol; ++q)
+      HIPCHK(hipMemcpyAsync(p->carry.as<float2>() + (size_t)q * nb, w + (size_t)q * total + input_idat,
+                            nb * sizeof(float2), hipMemcpyDeviceToDevice, s));
+  }
+  p->buffered = std::max<int64_t>(nb, 0);
+  if (mem == PFB_MEM_HOST) HIPCHK(hipStreamSynchronize(s));
+  return PFB_OK;
+}
+
+int64_t pfb_filterbank_buffered(const pfb_analysis_plan* p) { return p ? p->buffered : -1; }
+
+pfb_status pfb_filterbank_reset(pfb_analysis_plan* p) {
+  if (!p) return fail(PFB_ERR_INVALID_ARG, "null plan");
+  p->buffered = 0;
+  return PFB_OK;
+}
+
+}  // extern "C"
+
+// ====================================================================== synthesis plan
+struct pfb_synthesis_plan {
+  int device = 0;
+  int N = 0, nu = 1, de = 1, Nf = 0, Ov = 0, spans = 1, combine = 1, n_pol = 1;
+  int W = 0, keep = 0, L = 0, Lov = 0, Lkeep = 0, t1_lo = 0, t1_hi = 0;
+  bool deripple = false;
+  int chunk_blocks = 0;
+  bool identity_perm = true;
+  bool has_cgain = false;
+  DevBuf window, src, gain, expo, twL, twN, twNf, twW, perm, cgain;
+  DevBuf Z, carry, work, stage_in, stage_out;
+  int64_t buffered = 0;
+};
+
+static void hann_sym(int L, std::vector<double>& h) {
+  h.resize((size_t)L);
+  if (L == 1) {
+    h[0] = 1.0;
+    return;
+  }
+  for (int n = 0; n < L; ++n) h[(size_t)n] = 0.5 * (1.0 - std::cos(2.0 * M_PI * n / (L - 1)));
+}
+
+static int64_t synth_blocks(const pfb_synthesis_plan* p, int64_t n_dat) {
+  const int64_t b = floordiv(n_dat - 2 * (int64_t)p->Ov, p->keep);
+  return std::max<int64_t>(b, 0);
+}
+
+static pfb_status synthesis_run(pfb_synthesis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
+                                float2* out, int64_t out_ps, int64_t out_limit, hipStream_t s) {
+  const int64_t B = synth_blocks(p, n_dat);
+  if (B == 0) return PFB_OK;
+  int64_t CB = p->chunk_blocks;
+  if (CB <= 0) {
+    const int64_t target = (int64_t)1 << 22;  // ~32 MB of Z per chunk
+    CB = std::max<int64_t>(1, target / ((int64_t)p->keep * p->N * p->n_pol));
+  }
+  CB = std::min<int64_t>(CB, B);
+  const int64_t zrows = CB * p->keep + 2 * (int64_t)p->Ov;
+  HIPCHK(p->Z.ensure((size_t)p->n_pol * zrows * p->N * sizeof(float2)));
+  float2* Z = p->Z.as<float2>();
+  for (int64_t b0 = 0; b0 < B; b0 += CB) {
+    const int64_t nb = std::min<int64_t>(CB, B - b0);
+    const int64_t rows = nb * p->keep + 2 * (int64_t)p->Ov;
+    pfb::ChanIfftArgs c{};
+    c.in = in + b0 * p->keep * p->N;
+    c.in_pol_stride = in_ps;
+    c.out = Z;
+    c.out_pol_stride = zrows * p->N;
+    c.n_rows = rows;
+    c.n_pol = p->n_pol;
+    c.N = p->N;
+    c.perm = p->identity_perm ? nullptr : p->perm.as<int>();
+    c.cgain = p->has_cgain ? p->cgain.as<float>() : nullptr;
+    c.twN = p->twN.as<float2>();
+    {
+      ProfScope ps(1, (double)p->n_pol * rows * p->N * 16.0, s);
+      HIPCHK(pfb::launch_chan_ifft(c, s));
+    }
+    pfb::SynthBlockArgs a{};
+    a.Z = Z;
+    a.z_pol_stride = zrows * p->N;
+    a.out = out;
+    a.out_pol_stride = out_ps;
+    a.block0 = b0;
+    a.n_blocks = (int)nb;
+    a.n_pol = p->n_pol;
+    a.N = p->N;
+    a.Nf = p->Nf;
+    a.W = p->W;
+    a.keep = p->keep;
+    a.L = p->L;
+    a.Lov = p->Lov;
+    a.Lkeep = p->Lkeep;
+    a.t1_lo = p->t1_lo;
+    a.t1_hi = p->t1_hi;
+    a.scale = (float)((double)p->de / (double)p->nu / (double)p->L);
+    a.window = p->window.as<float>();
+    a.src = p->src.as<int>();
+    a.gain = p->gain.as<float>();
+    a.expo = p->expo.as<int>();
+    a.twL = p->twL.as<float2>();
+    a.twNf = p->twNf.as<float2>();
+    a.twW = p->twW.as<float2>();
+    a.out_limit = out_limit;
+    {
+      ProfScope ps(2, (double)p->n_pol * (nb * p->keep * p->N * 8.0 + nb * p->Lkeep * 8.0), s);
+      HIPCHK(pfb::launch_synth_block(a, s));
+    }
+  }
+  return PFB_OK;
+}
+
+extern "C" {
+
+pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_plan** out) {
+  if (!d || !out) return fail(PFB_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  const int N = d->n_chan, nu = d->os_nu, de = d->os_de, Nf = d->input_fft_length,
+            Ov = d->input_overlap;
+  if (N <= 0 || nu <= 0 || de <= 0 || Nf <= 0 || Ov < 0 || d->n_pol <= 0)
+    return fail(PFB_ERR_INVALID_ARG, "invalid synthesis parameters");
+  if (((int64_t)Nf * de) % nu != 0)
+    return fail(PFB_ERR_INVALID_ARG, "input_fft_length*de/nu = %d*%d/%d is not integral", Nf, de, nu);
+  if (((int64_t)Ov * de * N) % nu != 0)
+    return fail(PFB_ERR_INVALID_ARG, "output_overlap = Ov*de/nu*n_chan is not integral");
+  if (Nf - 2 * Ov <= 0) return fail(PFB_ERR_INVALID_ARG, "input_keep = Nf - 2 Ov must be positive");
+  const int W = (int)(((int64_t)Nf * de) / nu);
+  if (W % 2 != 0) return fail(PFB_ERR_INVALID_ARG, "FN_width %d must be even", W);
+  if (d->combine < 1 || N % d->combine != 0)
+    return fail(PFB_ERR_INVALID_ARG, "combine=%d must divide n_chan=%d", d->combine, N);
+  if (d->spectral_taper != PFB_WINDOW_NONE)
+    return fail(PFB_ERR_UNSUPPORTED,
+                "non-identity spectral taper is not implemented on the GPU path yet");
+  if (!pfb::chan_ifft_supported(N))
+    return fail(PFB_ERR_UNSUPPORTED, "no channel-IFFT kernel for n_chan=%d", N);
+  if (!pfb::synth_block_supported(Nf, W))
+    return fail(PFB_ERR_UNSUPPORTED, "no synthesis kernel for Nf=%d W=%d", Nf, W);
+  if ((int64_t)W * N >= (1LL << 30)) return fail(PFB_ERR_UNSUPPORTED, "L too large");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(PFB_ERR_NO_DEVICE, "no HIP device available");
+  if (d->device < 0 || d->device >= ndev)
+    return fail(PFB_ERR_INVALID_ARG, "device %d out of range", d->device);
+  HIPCHK(hipSetDevice(d->device));
+
+  auto* p = new pfb_synthesis_plan();
+  p->device = d->device;
+  p->N = N;
+  p->nu = nu;
+  p->de = de;
+  p->Nf = Nf;
+  p->Ov = Ov;
+  p->spans = d->spans_nyquist ? 1 : 0;
+  p->combine = d->combine;
+  p->n_pol = d->n_pol;
+  p->W = W;
+  p->keep = Nf - 2 * Ov;
+  p->L = W * N;
+  p->Lov = (int)(((int64_t)Ov * de * N) / nu);
+  p->Lkeep = p->L - 2 * p->Lov;
+  // L_ov = Ov*de/nu*N is a multiple of N when Ov*de/nu is integral; the block kernel
+  // emits y[t0 + N t1] for t1 in [t1_lo, t1_hi)
+  if (p->Lov % N != 0) {
+    delete p;
+    return fail(PFB_ERR_UNSUPPORTED, "output_overlap not a multiple of n_chan");
+  }
+  p->t1_lo = p->Lov / N;
+  p->t1_hi = W - p->t1_lo;
+  p->deripple = d->apply_deripple != 0;
+
+  // temporal taper (PFBWindow.m) -> per-time window + per-channel gain (hann quirk)
+  std::vector<float> window((size_t)Nf, 1.f);
+  std::vector<float> cgain;
+  switch (d->temporal_taper) {
+    case PFB_WINDOW_NONE: break;
+    case PFB_WINDOW_TUKEY: {
+      std::vector<double> h;
+      hann_sym(2 * Ov, h);
+      for (int t = 0; t < Ov; ++t) window[(size_t)t] = (float)h[(size_t)t];
+      for (int t = 0; t < Ov; ++t) window[(size_t)(Nf - Ov + t)] = (float)h[(size_t)(Ov + t)];
+      break;
+    }
+    case PFB_WINDOW_TOP_HAT:
+      for (int t = 0; t < Ov; ++t) {
+        window[(size_t)t] = 0.f;
+        window[(size_t)(Nf - 1 - t)] = 0.f;
+      }
+      break;
+    case PFB_WINDOW_HANN: {
+      // PFBWindow.m:72-99: hann along dim 1 = channels; circshift when n_chan != Nf
+      std::vector<double> h;
+      hann_sym(N, h);
+      cgain.resize((size_t)N);
+      for (int c = 0; c < N; ++c) {
+        const int src = (N != Nf) ? ((c - N / 2) % N + N) % N : c;
+        cgain[(size_t)c] = (float)h[(size_t)src];
+      }
+      break;
+    }
+    case PFB_WINDOW_CUSTOM:
+      if (!d->temporal_coeffs) {
+        delete p;
+        return fail(PFB_ERR_INVALID_ARG, "CUSTOM temporal taper without coefficients");
+      }
+      for (int t = 0; t < Nf; ++t) window[(size_t)t] = (float)d->temporal_coeffs[t];
+      break;
+    default:
+      delete p;
+      return fail(PFB_ERR_INVALID_ARG, "unknown temporal taper %d", d->temporal_taper);
+  }
+
+  // combine permutation (polyphase_synthesis.m:198-239): slot chan <- input jchan
+  std::vector<int> perm((size_t)N);
+  for (int c = 0; c < N; ++c) perm[(size_t)c] = c;
+  if (p->combine > 1) {
+    const int fcc = N / p->combine, fco = N;
+    for (int chan = 0; chan < N; ++chan) {
+      int fine = (chan + fcc / 2) % fco;
+      int coarse = fine / fcc;
+      fine -= coarse * fcc;
+      coarse = (coarse + p->combine / 2) % p->combine;
+      fine = (fine + fcc / 2) % fcc;
+      perm[(size_t)chan] = coarse * fcc + fine;
+    }
+  }
+  for (int c = 0; c < N; ++c)
+    if (perm[(size_t)c] != c) p->identity_perm = false;
+
+  // kept-bin tables (see oracle.synthesis_tables and DESIGN.md)
+  const int W2 = W / 2, d2 = (Nf - W) / 2;
+  std::vector<double> g(W2 + 1, 1.0);
+  if (p->deripple) {
+    if (!d->taps || d->n_taps <= 0) {
+      delete p;
+      return fail(PFB_ERR_INVALID_ARG, "deripple requested without filter taps");
+    }
+    // H0 = freqz(h, 1, n), n = N*W/2; filter_response = 1/|H0(0..W/2)|  (:138-150)
+    const int64_t nfz = (int64_t)N * W2;
+    const int64_t two_n = 2 * nfz;
+    for (int k = 0; k <= W2; ++k) {
+      double re = 0.0, im = 0.0;
+      for (int64_t i = 0; i < d->n_taps; ++i) {
+        const int64_t m = ((int64_t)k * i) % two_n;  // angle = pi k i / n = 2 pi m / (2n)
+        const double a = 2.0 * M_PI * (double)m / (double)two_n;
+        re += d->taps[i] * std::cos(a);
+        im -= d->taps[i] * std::sin(a);
+      }
+      g[(size_t)k] = 1.0 / std::sqrt(re * re + im * im);
+    }
+  }
+  std::vector<int> src((size_t)W), expo((size_t)W);
+  std::vector<float> gain((size_t)W);
+  for (int jp = 0; jp < W; ++jp) {
+    int j, e;
+    if (p->spans) {
+      j = (jp + W2) % W;
+      e = (jp < W2) ? jp : jp - W;
+    } else {
+      j = jp;
+      e = jp;
+    }
+    src[(size_t)jp] = (d2 + j + Nf / 2) % Nf;
+    expo[(size_t)jp] = e;
+    gain[(size_t)jp] = (float)((j < W2) ? g[(size_t)(W2 - j)] : g[(size_t)(j - W2)]);
+  }
+  hipError_t e = upload(p->window, window);
+  if (e == hipSuccess) e = upload(p->src, src);
+  if (e == hipSuccess) e = upload(p->gain, gain);
+  if (e == hipSuccess) e = upload(p->expo, expo);
+  if (e == hipSuccess) e = upload(p->perm, perm);
+  if (e == hipSuccess && !cgain.empty()) {
+    e = upload(p->cgain, cgain);
+    p->has_cgain = true;
+  }
+  if (e == hipSuccess) e = upload(p->twL, twiddles(p->L, +1));
+  if (e == hipSuccess) e = upload(p->twN, twiddles(N, -1));
+  if (e == hipSuccess) e = upload(p->twNf, twiddles(Nf, -1));
+  if (e == hipSuccess) e = upload(p->twW, twiddles(W, -1));
+  if (e != hipSuccess) {
+    delete p;
+    return fail(PFB_ERR_HIP, "synthesis plan upload: %s", hipGetErrorString(e));
+  }
+  *out = p;
+  return PFB_OK;
+}
+
+pfb_status pfb_synthesis_plan_destroy(pfb_synthesis_plan* p) {
+  if (!p) return PFB_OK;
+  (void)hipSetDevice(p->device);
+  for (DevBuf* b : {&p->window, &p->src, &p->gain, &p->expo, &p->twL, &p->twN, &p->twNf, &p->twW,
+                    &p->perm, &p->cgain, &p->Z, &p->carry, &p->work, &p->stage_in, &p->stage_out})
+    b->release();
+  delete p;
+  return PFB_OK;
+}
+
+int64_t pfb_synthesis_output_length(const pfb_synthesis_plan* p, int64_t n_dat) {
+  if (!p) return -1;
+  return synth_blocks(p, n_dat) * p->Lkeep;
+}
+
+pfb_status pfb_synthesis_set_chunk_blocks(pfb_synthesis_plan* p, int32_t blocks) {
+  if (!p) return fail(PFB_ERR_INVALID_ARG, "null plan");
+  p->chunk_blocks = std::max(0, blocks);
+  return PFB_OK;
+}
+
+pfb_status pfb_synthesis_execute(pfb_synthesis_plan* p, const pfb_cf32* in, int64_t in_ps,
+                                 int64_t n_dat, int64_t sample_offset, pfb_cf32* out,
+                                 int64_t out_ps, int64_t cap, int64_t* n_out, int32_t mem,
+                                 void* stream) {
+  if (!p || (!in && n_dat > 0)) return fail(PFB_ERR_INVALID_ARG, "null argument");
+  if (sample_offset < 1) return fail(PFB_ERR_INVALID_ARG, "sample_offset is 1-based (>= 1)");
+  HIPCHK(hipSetDevice(p->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t off = std::min<int64_t>(sample_offset - 1, std::max<int64_t>(n_dat, 0));
+  const int64_t n = n_dat - off;  // in = in(:, :, sample_offset:end)  (:99)
+  const int64_t olen = synth_blocks(p, n) * p->Lkeep;
+  if (n_out) *n_out = olen;
+  if (olen == 0) return PFB_OK;
+  if (!out) return fail(PFB_ERR_INVALID_ARG, "null output");
+  if (cap < olen) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld",
+                              (long long)cap, (long long)olen);
+  if (mem == PFB_MEM_DEVICE) {
+    if (in_ps < n_dat * p->N || out_ps < olen)
+      return fail(PFB_ERR_INVALID_ARG, "polarisation stride smaller than the data");
+    return synthesis_run(p, (const float2*)in + off * p->N, in_ps, n, (float2*)out, out_ps, olen, s);
+  }
+  HIPCHK(p->stage_in.ensure((size_t)p->n_pol * n * p->N * sizeof(float2)));
+  HIPCHK(p->stage_out.ensure((size_t)p->n_pol * olen * sizeof(float2)));
+  for (int q = 0; q < p->n_pol; ++q)
+    HIPCHK(hipMemcpyAsync(p->stage_in.as<float2>() + (size_t)q * n * p->N, in + q * in_ps + off * p->N,
+                          n * p->N * sizeof(float2), hipMemcpyHostToDevice, s));
+  pfb_status st = synthesis_run(p, p->stage_in.as<float2>(), n * p->N, n, p->stage_out.as<float2>(),
+                                olen, olen, s);
+  if (st != PFB_OK) return st;
+  for (int q = 0; q < p->n_pol; ++q)
+    HIPCHK(hipMemcpyAsync(out + q * out_ps, p->stage_out.as<float2>() + (size_t)q * olen,
+                          olen * sizeof(float2), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return PFB_OK;
+}
+
+pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* p, const pfb_cf32* in, int64_t in_ps,
+                                          int64_t n_in, pfb_cf32* out, int64_t out_ps, int64_t cap,
+                                          int64_t* n_out, int32_t mem, void* stream) {
+  if (!p || (!in && n_in > 0)) return fail(PFB_ERR_INVALID_ARG, "null argument");
+  HIPCHK(hipSetDevice(p->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int N = p->N;
+  const int64_t total = p->buffered + n_in;
+  const hipMemcpyKind kin = mem == PFB_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  HIPCHK(p->work.ensure((size_t)p->n_pol * std::max<int64_t>(total, 1) * N * sizeof(float2)));
+  float2* w = p->work.as<float2>();
+  for (int q = 0; q < p->n_pol; ++q) {
+    if (p->buffered > 0)
+      HIPCHK(hipMemcpyAsync(w + (size_t)q * total * N, p->carry.as<float2>() + (size_t)q * p->buffered * N,
+                            p->buffered * N * sizeof(float2), hipMemcpyDeviceToDevice, s));
+    if (n_in > 0)
+      HIPCHK(hipMemcpyAsync(w + (size_t)q * total * N + p->buffered * N, in + q * in_ps,
+                            n_in * N * sizeof(float2), kin, s));
+  }
+  // output length and carry-over rounded up to a multiple of nu (InverseFilterBank.m:104-135)
+  const int64_t B = synth_blocks(p, total);
+  const int64_t full = B * p->Lkeep;
+  int64_t input_idat = B * p->keep;
+  int64_t buffered = total - input_idat;
+  int64_t olen = full;
+  const int64_t rem = ((buffered % p->nu) + p->nu) % p->nu;
+  if (rem != 0) {
+    buffered += p->nu - rem;
+    input_idat = total - buffered;
+    // output_ndat = input_idat * (n_chan de)/nu, used as a Matlab colon end (floor)
+    olen = std::max<int64_t>(0, floordiv(input_idat * N * p->de, p->nu));
+    olen = std::min(olen, full);
+  }
+  if (n_out) *n_out = olen;
+  if (olen > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld",
+                              (long long)cap, (long long)olen);
+  if (olen > 0) {
+    if (mem == PFB_MEM_HOST) {
+      HIPCHK(p->stage_out.ensure((size_t)p->n_pol * olen * sizeof(float2)));
+      pfb_status st = synthesis_run(p, w, total * N, total, p->stage_out.as<float2>(), olen, olen, s);
+      if (st != PFB_OK) return st;
+      for (int q = 0; q < p->n_pol; ++q)
+        HIPCHK(hipMemcpyAsync(out + q * out_ps, p->stage_out.as<float2>() + (size_t)q * olen,
+                              olen * sizeof(float2), hipMemcpyDeviceToHost, s));
+    } else {
+      pfb_status st = synthesis_run(p, w, total * N, total, (float2*)out, out_ps, olen, s);
+      if (st != PFB_OK) return st;
+    }
+  }
+  if (buffered > 0) {
+    HIPCHK(p->carry.ensure((size_t)p->n_pol * buffered * N * sizeof(float2)));
+    for (int q = 0; q < p->n_pol; ++q)
+      HIPCHK(hipMemcpyAsync(p->carry.as<float2>() + (size_t)q * buffered * N,
+                            w + (size_t)q * total * N + input_idat * N, buffered * N * sizeof(float2),
+                            hipMemcpyDeviceToDevice, s));
+  }
+  p->buffered = std::max<int64_t>(buffered, 0);
+  if (mem == PFB_MEM_HOST) HIPCHK(hipStreamSynchronize(s));
+  return PFB_OK;
+}
+
+int64_t pfb_inverse_filterbank_buffered(const pfb_synthesis_plan* p) { return p ? p->buffered : -1; }
+
+pfb_status pfb_inverse_filterbank_reset(pfb_synthesis_plan* p) {
+  if (!p) return fail(PFB_ERR_INVALID_ARG, "null plan");
+  p->buffered = 0;
+  return PFB_OK;
+}
+
+// ------------------------------------------------------------------ utilities
+pfb_status pfb_device_malloc(int32_t device, int64_t bytes, void** ptr) {
+  if (!ptr || bytes < 0) return fail(PFB_ERR_INVALID_ARG, "bad arguments");
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipMalloc(ptr, (size_t)std::max<int64_t>(bytes, 1)));
+  return PFB_OK;
+}
+pfb_status pfb_device_free(void* ptr) {
+  if (ptr) HIPCHK(hipFree(ptr));
+  return PFB_OK;
+}
+pfb_status pfb_memcpy_h2d(void* dst, const void* src, int64_t bytes, void* stream) {
+  HIPCHK(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return PFB_OK;
+}
+pfb_status pfb_memcpy_d2h(void* dst, const void* src, int64_t bytes, void* stream) {
+  HIPCHK(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return PFB_OK;
+}
+pfb_status pfb_stream_synchronize(void* stream) {
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return PFB_OK;
+}
+
+pfb_status pfb_profile_enable(int32_t enable) {
+  g_prof.drain();
+  g_prof.enabled = enable != 0;
+  return PFB_OK;
+}
+pfb_status pfb_profile_read(int32_t which, double* total_ms, int64_t* launches, double* bytes) {
+  if (which < 0 || which > 2) return fail(PFB_ERR_INVALID_ARG, "which must be 0..2");
+  g_prof.drain();
+  if (total_ms) *total_ms = g_prof.total_ms[which];
+  if (launches) *launches = g_prof.launches[which];
+  if (bytes) *bytes = g_prof.bytes[which];
+  return PFB_OK;
+}
+pfb_status pfb_profile_reset(void) {
+  g_prof.drain();
+  for (int i = 0; i < 3; ++i) {
+    g_prof.total_ms[i] = 0;
+    g_prof.launches[i] = 0;
+    g_prof.bytes[i] = 0;
+  }
+  return PFB_OK;
+}
+
+}  // extern "C"

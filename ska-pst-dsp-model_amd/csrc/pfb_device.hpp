@@ -1,0 +1,313 @@
+// pfb_device.hpp — CDNA4 (gfx950) device building blocks for the PFB kernels.
+//
+// * complex float32 helpers (float2, interleaved re/im like pfb_cf32)
+// * register-resident small DFTs of any radix built from {2,3,4,5,7} by a
+//   compile-time Cooley-Tukey split; twiddles are compile-time constants
+//   computed in double (constexpr Taylor series) and rounded once to float
+// * an LDS-resident mixed-radix Stockham pass that a whole workgroup applies to a
+//   batch of rows; loads/stores of the first/last pass can be redirected to HBM
+//   through functors so the FFT fuses with its producer/consumer.
+//
+// The transforms here are bandwidth-shaped (complex-float VALU butterflies, LDS
+// exchange between passes); there is no dense contraction, so no MFMA.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+#include <utility>
+
+namespace pfb {
+
+// ------------------------------------------------------------------ complex helpers
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+// a * conj(b)
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, a.y * b.y), fmaf(a.y, b.x, -a.x * b.y));
+}
+// a * e^{DIR * i pi/2}: DIR=-1 -> -i*a, DIR=+1 -> +i*a
+template <int DIR>
+__device__ __forceinline__ float2 crot90(float2 a) {
+  if constexpr (DIR < 0) return make_float2(a.y, -a.x);
+  else return make_float2(-a.y, a.x);
+}
+
+// ------------------------------------------------------------------ constexpr trig
+constexpr double kPi = 3.14159265358979323846264338327950288;
+
+constexpr double taylor_sin(double x) {
+  double term = x, sum = x;
+  for (int i = 1; i < 24; ++i) {
+    term *= -x * x / ((2.0 * i) * (2.0 * i + 1.0));
+    sum += term;
+  }
+  return sum;
+}
+constexpr double taylor_cos(double x) {
+  double term = 1.0, sum = 1.0;
+  for (int i = 1; i < 24; ++i) {
+    term *= -x * x / ((2.0 * i - 1.0) * (2.0 * i));
+    sum += term;
+  }
+  return sum;
+}
+// cos/sin of 2 pi m / R, exact rational reduction into [-pi, pi]
+constexpr double cos2pi(long m, long R) {
+  m %= R;
+  if (m < 0) m += R;
+  if (2 * m > R) m -= R;
+  return taylor_cos(2.0 * kPi * double(m) / double(R));
+}
+constexpr double sin2pi(long m, long R) {
+  m %= R;
+  if (m < 0) m += R;
+  if (2 * m > R) m -= R;
+  return taylor_sin(2.0 * kPi * double(m) / double(R));
+}
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// multiply by the compile-time twiddle e^{DIR * 2 pi i M / R}
+template <int M, int R, int DIR>
+__device__ __forceinline__ float2 ctw(float2 a) {
+  if constexpr ((M % R) == 0) {
+    return a;
+  } else if constexpr ((4 * M) % R == 0) {
+    constexpr int q = ((4 * M) / R) % 4;  // multiples of pi/2
+    if constexpr (q == 2) return make_float2(-a.x, -a.y);
+    else if constexpr (q == 1) return crot90<DIR>(a);
+    else return crot90<-DIR>(a);
+  } else {
+    constexpr float c = (float)cos2pi(M, R);
+    constexpr float s = (float)(DIR * sin2pi(M, R));
+    return make_float2(fmaf(a.x, c, -a.y * s), fmaf(a.x, s, a.y * c));
+  }
+}
+
+// ------------------------------------------------------------------ small DFTs
+constexpr int first_factor(int R) {
+  if (R % 4 == 0 && R != 8) return 4;
+  if (R % 2 == 0) return 2;
+  if (R % 3 == 0) return 3;
+  if (R % 5 == 0) return 5;
+  if (R % 7 == 0) return 7;
+  return R;
+}
+
+// In-place DFT of R points held in registers, natural order in and out.
+// DIR = -1: X[k] = sum x[n] e^{-2 pi i n k / R}; DIR = +1: unnormalised inverse.
+template <int R, int DIR>
+__device__ __forceinline__ void sdft(float2* v) {
+  if constexpr (R == 1) {
+    return;
+  } else if constexpr (R == 2) {
+    float2 a = v[0];
+    v[0] = cadd(a, v[1]);
+    v[1] = csub(a, v[1]);
+  } else if constexpr (R == 3) {
+    constexpr float c = -0.5f;
+    constexpr float s = (float)(DIR * 0.86602540378443864676372317075294);
+    float2 t = cadd(v[1], v[2]);
+    float2 d = csub(v[1], v[2]);
+    float2 m = make_float2(fmaf(c, t.x, v[0].x), fmaf(c, t.y, v[0].y));
+    // d * i s
+    float2 ids = make_float2(-s * d.y, s * d.x);
+    v[0] = cadd(v[0], t);
+    v[1] = cadd(m, ids);
+    v[2] = csub(m, ids);
+  } else if constexpr (R == 4) {
+    float2 t0 = cadd(v[0], v[2]);
+    float2 t1 = csub(v[0], v[2]);
+    float2 t2 = cadd(v[1], v[3]);
+    float2 t3 = crot90<DIR>(csub(v[1], v[3]));
+    v[0] = cadd(t0, t2);
+    v[2] = csub(t0, t2);
+    v[1] = cadd(t1, t3);
+    v[3] = csub(t1, t3);
+  } else if constexpr (R == 5 || R == 7) {
+    // direct symmetric form: pairs (n, R-n)
+    constexpr int H = (R - 1) / 2;
+    float2 sp[H], sm[H];
+    static_for<0, H>([&](auto n) {
+      sp[n] = cadd(v[n + 1], v[R - 1 - n]);
+      sm[n] = csub(v[n + 1], v[R - 1 - n]);
+    });
+    float2 out[R];
+    float2 x0 = v[0];
+    float2 dc = x0;
+    static_for<0, H>([&](auto n) { dc = cadd(dc, sp[n]); });
+    out[0] = dc;
+    static_for<1, H + 1>([&](auto k) {
+      float2 re = x0;  // real-cos part
+      float2 im = make_float2(0.f, 0.f);
+      static_for<0, H>([&](auto n) {
+        constexpr int nk = (decltype(n)::value + 1) * decltype(k)::value;
+        constexpr float c = (float)cos2pi(nk, R);
+        constexpr float s = (float)sin2pi(nk, R);
+        re.x = fmaf(c, sp[n].x, re.x);
+        re.y = fmaf(c, sp[n].y, re.y);
+        im.x = fmaf(s, sm[n].x, im.x);
+        im.y = fmaf(s, sm[n].y, im.y);
+      });
+      // X[k] = re + DIR * i * im ; X[R-k] = re - DIR * i * im
+      float2 iim = make_float2(-im.y, im.x);  // i * im
+      if constexpr (DIR < 0) {
+        out[k] = csub(re, iim);
+        out[R - k] = cadd(re, iim);
+      } else {
+        out[k] = cadd(re, iim);
+        out[R - k] = csub(re, iim);
+      }
+    });
+    static_for<0, R>([&](auto k) { v[k] = out[k]; });
+  } else {
+    constexpr int A = first_factor(R);
+    constexpr int B = R / A;
+    static_assert(A * B == R && A > 1 && B > 1, "unsupported radix");
+    float2 y[A][B];
+    static_for<0, A>([&](auto n1) {
+      static_for<0, B>([&](auto n2) { y[n1][n2] = v[A * n2 + n1]; });
+      sdft<B, DIR>(y[n1]);
+      static_for<1, B>([&](auto k1) {
+        constexpr int m = decltype(n1)::value * decltype(k1)::value;
+        y[n1][k1] = ctw<m, R, DIR>(y[n1][k1]);
+      });
+    });
+    static_for<0, B>([&](auto k1) {
+      float2 z[A];
+      static_for<0, A>([&](auto n1) { z[n1] = y[n1][k1]; });
+      sdft<A, DIR>(z);
+      static_for<0, A>([&](auto k2) { v[k1 + B * k2] = z[k2]; });
+    });
+  }
+}
+
+// ------------------------------------------------------------------ LDS Stockham
+// Padded LDS index: one spare float2 every 16 breaks the power-of-two strides of
+// the radix-16 passes ("LDS layout").
+__device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
+__host__ __device__ constexpr int lds_row(int n) { return n + n / 16; }
+
+// Radix lists of the compiled transform sizes.
+template <int... Rs>
+struct Radices {};
+
+template <int N>
+struct FFTPlan;
+template <> struct FFTPlan<8> { using type = Radices<8>; };
+template <> struct FFTPlan<16> { using type = Radices<16>; };
+template <> struct FFTPlan<32> { using type = Radices<8, 4>; };
+template <> struct FFTPlan<64> { using type = Radices<8, 8>; };
+template <> struct FFTPlan<128> { using type = Radices<16, 8>; };
+template <> struct FFTPlan<256> { using type = Radices<16, 16>; };
+template <> struct FFTPlan<512> { using type = Radices<8, 8, 8>; };
+template <> struct FFTPlan<1024> { using type = Radices<16, 16, 4>; };
+template <> struct FFTPlan<2048> { using type = Radices<16, 16, 8>; };
+template <> struct FFTPlan<4096> { using type = Radices<16, 16, 16>; };
+// kept-bin widths W = Nf * de / nu of the synthesis
+template <> struct FFTPlan<96> { using type = Radices<16, 6>; };
+template <> struct FFTPlan<112> { using type = Radices<16, 7>; };
+template <> struct FFTPlan<192> { using type = Radices<16, 12>; };
+template <> struct FFTPlan<216> { using type = Radices<8, 27>; };
+template <> struct FFTPlan<224> { using type = Radices<16, 14>; };
+template <> struct FFTPlan<448> { using type = Radices<16, 28>; };
+template <> struct FFTPlan<896> { using type = Radices<16, 8, 7>; };
+
+// Default LDS accessors for a batch of rows stored at base + row * rs.
+struct LdsIO {
+  float2* base;
+  int rs;
+  __device__ __forceinline__ float2 load(int row, int i) const { return base[row * rs + lpad(i)]; }
+  __device__ __forceinline__ void store(int row, int i, float2 v) const { base[row * rs + lpad(i)] = v; }
+};
+
+// Twiddle e^{DIR 2 pi i m / N} from a table tw[m] = e^{-2 pi i m / N} (N entries).
+template <int DIR>
+__device__ __forceinline__ float2 table_tw(const float2* __restrict__ tw, int m) {
+  float2 w = tw[m];
+  if constexpr (DIR > 0) w.y = -w.y;
+  return w;
+}
+
+// One Stockham autosort pass of radix R over `rows` transforms of length N held by
+// the workgroup.  NS = product of the radices already applied.  Loads through `in`,
+// stores through `out`.  All NT threads participate; the pass contains one barrier
+// between its loads and its stores, so `in` and `out` may alias (in-place via
+// registers).  The caller places a barrier before the next pass reads `out`.
+template <int N, int R, int NS, int DIR, int ROWS, int NT, class In, class Out>
+__device__ __forceinline__ void stockham_pass(const In& in, const Out& out,
+                                              const float2* __restrict__ tw, int tid) {
+  constexpr int NB = N / R;
+  constexpr int TOT = ROWS * NB;
+  constexpr int PER = (TOT + NT - 1) / NT;
+  float2 v[PER][R];
+  static_for<0, PER>([&](auto p) {
+    const int b = tid + p * NT;
+    if (TOT % NT == 0 || b < TOT) {
+      const int row = b / NB, j = b - (b / NB) * NB;
+      static_for<0, R>([&](auto r) { v[p][r] = in.load(row, j + r * NB); });
+    }
+  });
+  if constexpr (In::kIsLds && Out::kIsLds) __syncthreads();
+  static_for<0, PER>([&](auto p) {
+    const int b = tid + p * NT;
+    if (TOT % NT == 0 || b < TOT) {
+      const int row = b / NB, j = b - (b / NB) * NB;
+      const int k = j % NS;
+      if constexpr (NS > 1) {
+        static_for<1, R>([&](auto r) {
+          // e^{DIR 2 pi i r k / (NS R)} = table[(r k N / (NS R))]
+          v[p][r] = cmul(v[p][r], table_tw<DIR>(tw, r * k * (N / (NS * R))));
+        });
+      }
+      sdft<R, DIR>(v[p]);
+      const int idxD = (j / NS) * NS * R + k;
+      static_for<0, R>([&](auto r) { out.store(row, idxD + r * NS, v[p][r]); });
+    }
+  });
+}
+
+// LDS row accessor (in-place passes need a barrier between loads and stores).
+struct LdsRows : LdsIO {
+  static constexpr bool kIsLds = true;
+  __device__ LdsRows(float2* b, int r) : LdsIO{b, r} {}
+};
+
+// Run all passes of FFTPlan<N>; first pass loads via `first`, last pass stores via
+// `last`, intermediate passes go through the LDS rows `lds`.
+template <int N, int DIR, int ROWS, int NT, int NS, int R, int... Rest, class First, class Last>
+__device__ __forceinline__ void run_passes_impl(const First& first, const Last& last,
+                                                const LdsRows& lds, const float2* tw, int tid) {
+  if constexpr (sizeof...(Rest) == 0) {
+    stockham_pass<N, R, NS, DIR, ROWS, NT>(first, last, tw, tid);
+  } else {
+    stockham_pass<N, R, NS, DIR, ROWS, NT>(first, lds, tw, tid);
+    __syncthreads();
+    run_passes_impl<N, DIR, ROWS, NT, NS * R, Rest...>(lds, last, lds, tw, tid);
+  }
+}
+
+template <int N, int DIR, int ROWS, int NT, class First, class Last, int... Rs>
+__device__ __forceinline__ void run_fft(const First& first, const Last& last, const LdsRows& lds,
+                                        const float2* tw, int tid, Radices<Rs...>) {
+  run_passes_impl<N, DIR, ROWS, NT, 1, Rs...>(first, last, lds, tw, tid);
+}
+
+template <int N, int DIR, int ROWS, int NT, class First, class Last>
+__device__ __forceinline__ void block_fft(const First& first, const Last& last, const LdsRows& lds,
+                                          const float2* tw, int tid) {
+  run_fft<N, DIR, ROWS, NT>(first, last, lds, tw, tid, typename FFTPlan<N>::type{});
+}
+
+}  // namespace pfb

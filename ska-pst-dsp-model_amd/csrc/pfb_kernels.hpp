@@ -1,0 +1,73 @@
+// pfb_kernels.hpp — internal (C++) launcher interface between the C ABI and the
+// HIP kernels.  Not part of the public boundary (see include/pfb_api.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pfb {
+
+enum Variant { kBunton = 0, kPadded = 1 };
+
+// Polyphase analysis (polyphase_analysis.m / polyphase_analysis_padded.m).
+struct AnalysisArgs {
+  const float2* in;        // [pol][t]
+  int64_t in_pol_stride;
+  int64_t n_dat;
+  float2* out;             // [pol][k][c]
+  int64_t out_pol_stride;
+  int64_t K;               // output rows per pol
+  int n_pol;
+  int N, M, P, nu, sds;    // channels, step, phases, os numerator, padded delay shift
+  int variant;
+  const float* taps;       // P*N padded taps (device)
+  const float2* twN;       // e^{-2 pi i m / N}, m < N (device)
+  float2* scratch;         // generic path: [pol][K][N] (device) or null
+};
+
+// Synthesis stage 1: per channelised time row, N-point inverse DFT across channels
+// (after the combine permutation and per-channel gain).  See DESIGN.md §synthesis.
+struct ChanIfftArgs {
+  const float2* in;        // [pol][row][c], rows already offset to the first row
+  int64_t in_pol_stride;
+  float2* out;             // Z: [pol][row][t0]
+  int64_t out_pol_stride;
+  int64_t n_rows;
+  int n_pol;
+  int N;
+  const int* perm;         // slot -> input channel (null = identity)
+  const float* cgain;      // per-slot gain (null = 1)
+  const float2* twN;
+};
+
+// Synthesis stage 2: per block and group of t0, Nf-point FFT over time, kept-bin
+// selection with deripple gain and four-step twiddle, W-point inverse FFT,
+// overlap-discard and the 1/L * de/nu scale.
+struct SynthBlockArgs {
+  const float2* Z;         // [pol][row][t0] (chunk-local rows)
+  int64_t z_pol_stride;
+  float2* out;             // [pol][t]
+  int64_t out_pol_stride;
+  int64_t block0;          // global index of the chunk's first block
+  int n_blocks;            // blocks in this chunk
+  int n_pol;
+  int N, Nf, W, keep, L, Lov, Lkeep, t1_lo, t1_hi;
+  float scale;
+  const float* window;     // Nf temporal window (device)
+  const int* src;          // W: source FFT bin
+  const float* gain;       // W: deripple gain
+  const int* expo;         // W: signed twiddle exponent
+  const float2* twL;       // e^{+2 pi i m / L}, m < L
+  const float2* twNf;      // e^{-2 pi i m / Nf}
+  const float2* twW;       // e^{-2 pi i m / W}
+  int64_t out_limit;       // samples per pol actually written (InverseFilterBank trim)
+};
+
+bool analysis_supported(int N, int P, int variant, bool* fused);
+hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s);
+bool chan_ifft_supported(int N);
+hipError_t launch_chan_ifft(const ChanIfftArgs& a, hipStream_t s);
+bool synth_block_supported(int Nf, int W);
+hipError_t launch_synth_block(const SynthBlockArgs& a, hipStream_t s);
+
+}  // namespace pfb

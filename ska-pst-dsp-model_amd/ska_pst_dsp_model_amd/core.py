@@ -1,0 +1,397 @@
+"""Plans and the Matlab-shaped functional API of the PFB hot path.
+
+    polyphase_analysis(in, filt, block, os_factor)          polyphase_analysis.m:1-7
+    polyphase_analysis_padded(in, filt, block, os_factor)   polyphase_analysis_padded.m:1-7
+    polyphase_synthesis(in, spans_nyq, Nf, os, deripple,
+                        sample_offset, overlap, t_taper,
+                        s_taper, combine)                    polyphase_synthesis.m:1-13
+
+Arrays follow the Matlab shapes: analysis input (n_pol, 1, n_dat), channelised data
+(n_pol, n_chan, n_dat), synthesis output (n_pol, 1, n_out).  Channelised arrays are
+returned as a transposed *view* of a (n_pol, n_dat, n_chan) buffer — the per-pol
+Matlab memory order (channel fastest), which is what the kernels read and write.
+
+Inputs may be NumPy arrays (host; the C ABI stages them through device buffers) or
+``torch`` tensors on a ROCm device (zero copy on the current stream).  Every call
+goes through the HIP kernels of ``libpfb_hip.so``; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+from ctypes import byref, c_int64, c_void_p
+
+import numpy as np
+
+from . import _lib
+from .config import Rational, as_rational
+from .window import PFBWindow, Taper, identity_taper
+
+__all__ = ["AnalysisPlan", "SynthesisPlan", "polyphase_analysis", "polyphase_analysis_padded",
+           "polyphase_synthesis", "analysis_plan", "synthesis_plan", "is_device_array"]
+
+
+def _torch():
+    try:
+        import torch  # noqa: F401
+        return torch
+    except Exception:  # pragma: no cover - torch is plumbing only
+        return None
+
+
+def is_device_array(x) -> bool:
+    t = _torch()
+    return t is not None and isinstance(x, t.Tensor) and x.is_cuda
+
+
+def _stream_of(x):
+    t = _torch()
+    return c_void_p(t.cuda.current_stream(x.device).cuda_stream)
+
+
+def _taps64(filt) -> np.ndarray:
+    if is_device_array(filt):
+        filt = filt.detach().cpu().numpy()
+    return np.ascontiguousarray(np.asarray(filt, dtype=np.float64).ravel())
+
+
+# ============================================================================ analysis
+class AnalysisPlan:
+    """Device plan of one analysis filter bank (owns taps, twiddles, carry-over)."""
+
+    def __init__(self, taps, n_chan: int, os_factor, variant: str = "polyphase_analysis",
+                 n_pol: int = 1, device: int = 0):
+        lib = _lib.load()
+        _lib.require_device()
+        self.os_factor = as_rational(os_factor)
+        self.n_chan = int(n_chan)
+        self.n_pol = int(n_pol)
+        self.device = int(device)
+        self.variant = variant
+        v = {"polyphase_analysis": _lib.PFB_ANALYSIS_BUNTON, "bunton": _lib.PFB_ANALYSIS_BUNTON,
+             "polyphase_analysis_padded": _lib.PFB_ANALYSIS_PADDED,
+             "padded": _lib.PFB_ANALYSIS_PADDED}
+        if variant not in v:
+            raise ValueError(f"unknown analysis function '{variant}'")
+        self.taps = _taps64(taps)
+        arr, ptr = _lib.c_double_array(self.taps)
+        d = _lib.AnalysisDesc(v[variant], self.n_chan, self.os_factor.nu, self.os_factor.de,
+                              ptr, len(arr), self.n_pol, self.device)
+        h = c_void_p()
+        _lib.check(lib.pfb_analysis_plan_create(byref(d), byref(h)))
+        self._h = h
+        self._lib = lib
+        self.step = (self.n_chan * self.os_factor.de) // self.os_factor.nu
+        self.phases = -(-len(self.taps) // self.n_chan)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.pfb_analysis_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def output_length(self, n_dat: int) -> int:
+        return int(self._lib.pfb_analysis_output_length(self._h, int(n_dat)))
+
+    @property
+    def buffered_samples(self) -> int:
+        return int(self._lib.pfb_filterbank_buffered(self._h))
+
+    def reset(self):
+        _lib.check(self._lib.pfb_filterbank_reset(self._h))
+
+    def _prep_in(self, x):
+        """-> (array (n_pol, n_dat) complex64 contiguous, is_device)."""
+        if is_device_array(x):
+            t = _torch()
+            x = x.to(t.complex64)
+            if x.dim() == 3:
+                x = x[:, 0, :]
+            elif x.dim() == 1:
+                x = x[None, :]
+            x = x.contiguous()
+            return x, True
+        x = np.asarray(x)
+        if x.ndim == 3:
+            x = x[:, 0, :]
+        elif x.ndim == 1:
+            x = x[None, :]
+        x = np.ascontiguousarray(x, dtype=np.complex64)
+        return x, False
+
+    def _alloc_out(self, like, dev, rows):
+        if dev:
+            t = _torch()
+            return t.empty((self.n_pol, max(rows, 0), self.n_chan), dtype=t.complex64,
+                           device=like.device)
+        return np.empty((self.n_pol, max(rows, 0), self.n_chan), dtype=np.complex64)
+
+    def execute(self, x, stateful: bool = False):
+        """Run the analysis; returns the (n_pol, K, n_chan) buffer (time-major)."""
+        x, dev = self._prep_in(x)
+        if x.shape[0] != self.n_pol:
+            raise ValueError(f"plan built for n_pol={self.n_pol}, got {x.shape[0]}")
+        n_dat = x.shape[1]
+        if stateful:
+            cap = (self.buffered_samples + n_dat) // max(self.step, 1) + 1
+        else:
+            cap = self.output_length(n_dat)
+        out = self._alloc_out(x, dev, cap)
+        n_out = c_int64(0)
+        if dev:
+            src, dst, mem, stream = c_void_p(x.data_ptr()), c_void_p(out.data_ptr()), \
+                _lib.PFB_MEM_DEVICE, _stream_of(x)
+        else:
+            src, dst, mem, stream = x.ctypes.data_as(c_void_p), out.ctypes.data_as(c_void_p), \
+                _lib.PFB_MEM_HOST, c_void_p(0)
+        fn = self._lib.pfb_filterbank_execute if stateful else self._lib.pfb_analysis_execute
+        _lib.check(fn(self._h, src, n_dat, n_dat, dst, cap * self.n_chan, cap, byref(n_out),
+                      mem, stream))
+        return out[:, :n_out.value, :]
+
+
+# ============================================================================ synthesis
+def _resolve_taper(taper, nf: int, ov: int):
+    """Translate a taper handle into (kind, coeffs) for the C ABI."""
+    if taper is None or taper is identity_taper:
+        return _lib.PFB_WINDOW_NONE, None
+    if isinstance(taper, str):
+        taper = PFBWindow().lookup[taper](nf, ov)
+    if isinstance(taper, Taper):
+        if taper.kind == _lib.PFB_WINDOW_CUSTOM:
+            return taper.kind, np.asarray(taper.coeffs, dtype=np.float64)
+        if taper.kind in (_lib.PFB_WINDOW_TUKEY, _lib.PFB_WINDOW_TOP_HAT) and \
+                (taper.input_fft_length, taper.input_discard) != (nf, ov):
+            # the Matlab handle closes over its own (Nf, Ov); honour them explicitly
+            return _lib.PFB_WINDOW_CUSTOM, taper.time_window(nf)
+        return taper.kind, None
+    kind = getattr(taper, "kind", None)
+    if kind == _lib.PFB_WINDOW_NONE:
+        return kind, None
+    raise TypeError("polyphase_synthesis: arbitrary Python taper callables cannot run on the "
+                    "GPU path; use a PFBWindow taper or PFBWindow().custom(coeffs)")
+
+
+def _resolve_deripple(deripple):
+    if deripple is None:
+        return False, None
+    if isinstance(deripple, dict):
+        return bool(deripple.get("apply_deripple", 0)), deripple.get("filter_coeff")
+    if isinstance(deripple, (tuple, list)):
+        return bool(deripple[0]), deripple[1]
+    if isinstance(deripple, (bool, int, np.bool_)):
+        return bool(deripple), None
+    return bool(getattr(deripple, "apply_deripple")), getattr(deripple, "filter_coeff", None)
+
+
+class SynthesisPlan:
+    """Device plan of one inverse filter bank (tables, twiddles, scratch, carry-over)."""
+
+    def __init__(self, n_chan: int, os_factor, input_fft_length: int, input_overlap: int = None,
+                 spans_nyquist: bool = True, combine: int = 1, deripple: bool = False,
+                 filter_coeff=None, temporal_taper=None, spectral_taper=None, n_pol: int = 1,
+                 device: int = 0):
+        lib = _lib.load()
+        _lib.require_device()
+        self.os_factor = as_rational(os_factor)
+        self.n_chan = int(n_chan)
+        self.input_fft_length = int(input_fft_length)
+        self.input_overlap = (self.input_fft_length // 8 if input_overlap is None
+                              else int(input_overlap))
+        self.n_pol = int(n_pol)
+        self.device = int(device)
+        nf, ov = self.input_fft_length, self.input_overlap
+        tk, tco = _resolve_taper(temporal_taper, nf, ov)
+        sk, sco = _resolve_taper(spectral_taper, nf, ov)
+        taps = _taps64(filter_coeff) if filter_coeff is not None else np.zeros(1)
+        self._keep = []
+        tarr, tptr = _lib.c_double_array(taps)
+        self._keep.append(tarr)
+        tcp = sco_p = None
+        if tco is not None:
+            a, tcp = _lib.c_double_array(tco)
+            self._keep.append(a)
+        if sco is not None:
+            a, sco_p = _lib.c_double_array(sco)
+            self._keep.append(a)
+        d = _lib.SynthesisDesc(self.n_chan, self.os_factor.nu, self.os_factor.de, nf, ov,
+                               1 if spans_nyquist else 0, int(combine), 1 if deripple else 0,
+                               tptr, len(tarr) if filter_coeff is not None else 0,
+                               tk, tcp, sk, sco_p, self.n_pol, self.device)
+        h = c_void_p()
+        _lib.check(lib.pfb_synthesis_plan_create(byref(d), byref(h)))
+        self._h = h
+        self._lib = lib
+        W = (nf * self.os_factor.de) // self.os_factor.nu
+        self.output_fft_length = W * self.n_chan
+        self.output_overlap = (ov * self.os_factor.de * self.n_chan) // self.os_factor.nu
+        self.output_keep = self.output_fft_length - 2 * self.output_overlap
+        self.input_keep = nf - 2 * ov
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.pfb_synthesis_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_chunk_blocks(self, blocks: int):
+        _lib.check(self._lib.pfb_synthesis_set_chunk_blocks(self._h, int(blocks)))
+
+    def output_length(self, n_dat: int) -> int:
+        return int(self._lib.pfb_synthesis_output_length(self._h, int(n_dat)))
+
+    @property
+    def buffered_samples(self) -> int:
+        return int(self._lib.pfb_inverse_filterbank_buffered(self._h))
+
+    def reset(self):
+        _lib.check(self._lib.pfb_inverse_filterbank_reset(self._h))
+
+    def _prep_in(self, x, layout: str):
+        """Accept (n_pol, n_chan, n_dat) Matlab-shaped or (n_pol, n_dat, n_chan) buffers."""
+        if is_device_array(x):
+            t = _torch()
+            x = x.to(t.complex64)
+            if layout == "pfc":
+                ptc = x.transpose(1, 2)
+            else:
+                ptc = x
+            return ptc.contiguous(), True
+        x = np.asarray(x)
+        ptc = x.transpose(0, 2, 1) if layout == "pfc" else x
+        return np.ascontiguousarray(ptc, dtype=np.complex64), False
+
+    def execute(self, x, sample_offset: int = 1, stateful: bool = False, layout: str = "pfc"):
+        """Run the synthesis; returns the (n_pol, n_out) series."""
+        ptc, dev = self._prep_in(x, layout)
+        if ptc.shape[0] != self.n_pol or ptc.shape[2] != self.n_chan:
+            raise ValueError(f"plan built for (n_pol={self.n_pol}, n_chan={self.n_chan}), "
+                             f"got {tuple(ptc.shape)} [pol, time, chan]")
+        n_dat = ptc.shape[1]
+        if stateful:
+            cap = self.output_length(self.buffered_samples + n_dat)
+        else:
+            cap = self.output_length(max(n_dat - (int(sample_offset) - 1), 0))
+        if dev:
+            t = _torch()
+            out = t.empty((self.n_pol, max(cap, 0)), dtype=t.complex64, device=ptc.device)
+            src, dst, mem, stream = c_void_p(ptc.data_ptr()), c_void_p(out.data_ptr()), \
+                _lib.PFB_MEM_DEVICE, _stream_of(ptc)
+        else:
+            out = np.empty((self.n_pol, max(cap, 0)), dtype=np.complex64)
+            src, dst, mem, stream = ptc.ctypes.data_as(c_void_p), out.ctypes.data_as(c_void_p), \
+                _lib.PFB_MEM_HOST, c_void_p(0)
+        n_out = c_int64(0)
+        if stateful:
+            _lib.check(self._lib.pfb_inverse_filterbank_execute(
+                self._h, src, n_dat * self.n_chan, n_dat, dst, cap, cap, byref(n_out), mem, stream))
+        else:
+            _lib.check(self._lib.pfb_synthesis_execute(
+                self._h, src, n_dat * self.n_chan, n_dat, int(sample_offset), dst, cap, cap,
+                byref(n_out), mem, stream))
+        return out[:, :n_out.value]
+
+
+# ============================================================================ plan cache
+_PLANS = {}
+
+
+def _key(*parts):
+    h = hashlib.sha1()
+    for p in parts:
+        if isinstance(p, np.ndarray):
+            h.update(p.tobytes())
+        else:
+            h.update(repr(p).encode())
+    return h.hexdigest()
+
+
+def analysis_plan(filt, block, os_factor, variant, n_pol, device=0) -> AnalysisPlan:
+    taps = _taps64(filt)
+    os_ = as_rational(os_factor)
+    k = _key("a", taps, int(block), str(os_), variant, int(n_pol), int(device))
+    p = _PLANS.get(k)
+    if p is None:
+        p = AnalysisPlan(taps, block, os_, variant, n_pol, device)
+        _PLANS[k] = p
+    return p
+
+
+def synthesis_plan(n_chan, os_factor, nf, ov, spans, combine, deripple, filt, t_taper, s_taper,
+                   n_pol, device=0) -> SynthesisPlan:
+    os_ = as_rational(os_factor)
+    tk, tco = _resolve_taper(t_taper, nf, ov)
+    sk, sco = _resolve_taper(s_taper, nf, ov)
+    taps = _taps64(filt) if (deripple and filt is not None) else None
+    k = _key("s", int(n_chan), str(os_), int(nf), int(ov), bool(spans), int(combine),
+             bool(deripple), taps if taps is not None else "-", tk,
+             tco if tco is not None else "-", sk, sco if sco is not None else "-",
+             int(n_pol), int(device))
+    p = _PLANS.get(k)
+    if p is None:
+        p = SynthesisPlan(n_chan, os_, nf, ov, spans, combine, deripple, taps, t_taper, s_taper,
+                          n_pol, device)
+        _PLANS[k] = p
+    return p
+
+
+def _device_of(x) -> int:
+    if is_device_array(x):
+        return x.device.index or 0
+    return 0
+
+
+def _pfc_view(buf):
+    """(n_pol, K, N) buffer -> Matlab-shaped (n_pol, N, K) view."""
+    if is_device_array(buf):
+        return buf.transpose(1, 2)
+    return buf.transpose(0, 2, 1)
+
+
+def _npol(x) -> int:
+    shape = tuple(x.shape)
+    return 1 if len(shape) == 1 else int(shape[0])
+
+
+# ============================================================================ functions
+def polyphase_analysis(in_, filt, block, os_factor, verbose_=0):
+    """polyphase_analysis.m:1-129 (Bunton).  Returns (n_pol, block, nblocks) complex64."""
+    plan = analysis_plan(filt, block, os_factor, "polyphase_analysis", _npol(in_),
+                         _device_of(in_))
+    return _pfc_view(plan.execute(in_))
+
+
+def polyphase_analysis_padded(in_, filt, block, os_factor, verbose_=0):
+    """polyphase_analysis_padded.m:1-161 (commutator).  Returns (n_pol, block, nblocks)."""
+    plan = analysis_plan(filt, block, os_factor, "polyphase_analysis_padded", _npol(in_),
+                         _device_of(in_))
+    return _pfc_view(plan.execute(in_))
+
+
+def polyphase_synthesis(in_, input_fully_spans_Nyquist_zone, input_fft_length, os_factor,
+                        deripple_=None, sample_offset_=1, input_overlap_=None,
+                        temporal_taper_=None, spectral_taper_=None, combine_=1, verbose_=0):
+    """polyphase_synthesis.m:1-325 (golden inversion).  Returns (n_pol, 1, n_out)."""
+    nf = int(input_fft_length)
+    ov = nf // 8 if input_overlap_ is None else int(input_overlap_)
+    dr, filt = _resolve_deripple(deripple_)
+    shape = tuple(in_.shape)
+    if len(shape) != 3:
+        raise ValueError("polyphase_synthesis input must be (n_pol, n_chan, n_dat)")
+    if not is_device_array(in_) and not np.iscomplexobj(np.asarray(in_)):
+        raise ValueError("polyphase_synthesis input data are real-valued!")
+    plan = synthesis_plan(shape[1], os_factor, nf, ov, bool(input_fully_spans_Nyquist_zone),
+                          int(combine_), dr, filt, temporal_taper_, spectral_taper_, shape[0],
+                          _device_of(in_))
+    out = plan.execute(in_, sample_offset=int(sample_offset_))
+    return out[:, None, :]

@@ -1,0 +1,318 @@
+"""GPU parity of the HIP kernels (through the C ABI) against the oracle.
+
+Sizes are chosen so the float64 oracle finishes in seconds; full BASELINE sizes are
+covered by size-independent properties in test_gpu_properties.py.
+Tolerance: the reference's np.isclose(atol=1e-6, rtol=1e-6) after dividing both
+sides by the oracle's peak magnitude (conftest.assert_pfb_close).
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_pfb_close
+from oracle import pfb_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _pfb():
+    import ska_pst_dsp_model_amd as pfb
+    return pfb
+
+
+def _taps(kind):
+    pfb = _pfb()
+    if kind == "test":
+        return pfb.design_PFB_FIR_filter(8, "8/7", 10)
+    if kind == "low87":
+        return pfb.design_PFB_FIR_filter(256, "8/7", 12)
+    if kind == "low43":
+        return pfb.design_PFB_FIR_filter(256, "4/3", 12)
+    if kind == "pst":
+        return pfb.read_fir_filter_coeff(pfb.config.config_dir + "/PST_filtertaps.txt")
+    if kind == "mid":
+        return pfb.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
+    raise KeyError(kind)
+
+
+def _noise(rng, shape):
+    return ((rng.standard_normal(shape) + 1j * rng.standard_normal(shape)) /
+            np.sqrt(2)).astype(np.complex64)
+
+
+def _tone(n, freq_bins, n_pol=1, phase=np.pi / 4):
+    t = np.arange(n)
+    x = np.exp(1j * (2 * np.pi * freq_bins / n * t + phase)).astype(np.complex64)
+    return np.repeat(x[None, None, :], n_pol, axis=0)
+
+
+# ----------------------------------------------------------------------------- analysis
+@pytest.mark.parametrize("case", [
+    ("test", 8, "8/7", 2, 4096, "bunton"),
+    ("low87", 256, "8/7", 1, 1 << 18, "bunton"),
+    ("low43", 256, "4/3", 2, 1 << 17, "bunton"),
+    ("pst", 256, "4/3", 1, 1 << 17, "bunton"),
+    ("test", 8, "8/7", 2, 4096, "padded"),
+    ("low87", 256, "8/7", 1, 1 << 17, "padded"),
+])
+def test_analysis_matches_oracle(gpu, case):
+    import torch
+    pfb = _pfb()
+    kind, N, os_, n_pol, n_dat, variant = case
+    taps = _taps(kind)
+    rng = np.random.default_rng(1234)
+    x = _noise(rng, (n_pol, 1, n_dat))
+    if variant == "bunton":
+        ref = orc.polyphase_analysis(x, taps, N, os_)
+        got = pfb.polyphase_analysis(torch.from_numpy(x).to(gpu), taps, N, os_)
+    else:
+        ref = orc.polyphase_analysis_padded(x, taps, N, os_)
+        got = pfb.polyphase_analysis_padded(torch.from_numpy(x).to(gpu), taps, N, os_)
+    assert_pfb_close(got.cpu().numpy(), ref, what=f"analysis {case}")
+
+
+def test_analysis_host_memory_path(gpu):
+    """PFB_MEM_HOST staging gives the same answer as device pointers."""
+    pfb = _pfb()
+    taps = _taps("test")
+    x = _noise(np.random.default_rng(7), (2, 1, 3000))
+    ref = orc.polyphase_analysis(x, taps, 8, "8/7")
+    got = pfb.polyphase_analysis(x, taps, 8, "8/7")
+    assert isinstance(got, np.ndarray)
+    assert_pfb_close(got, ref)
+
+
+def test_analysis_tone_closed_form(gpu):
+    """Known answer (polyphase_analysis.m:105-120 closed form): a tone x = e^{j w n}
+    gives out[c, k] = N e^{-j 2 pi c r_k / N} e^{j w M k} sum_i f[i] e^{j (w - 2 pi c / N) i}."""
+    import torch
+    pfb = _pfb()
+    N, M = 8, 7
+    taps = _taps("test")
+    n = 4096
+    w = 2 * np.pi * 0.0371
+    x = np.exp(1j * w * np.arange(n)).astype(np.complex64)[None, None, :]
+    got = pfb.polyphase_analysis(torch.from_numpy(x).to(gpu), taps, N, "8/7").cpu().numpy()[0]
+    f = orc.pad_filter(taps, N)
+    i = np.arange(len(f))
+    c = np.arange(N)
+    H = np.array([np.sum(f * np.exp(1j * (w - 2 * np.pi * cc / N) * i)) for cc in c])
+    K = got.shape[1]
+    k = np.arange(K)
+    r = (M * k) % N
+    ref = N * np.exp(-2j * np.pi * np.outer(c, r) / N) * np.exp(1j * w * M * k)[None, :] * H[:, None]
+    assert_pfb_close(got, ref, tol=2e-6)
+
+
+@pytest.mark.parametrize("N,os_,ppc", [(256, "32/27", 24), (64, "8/7", 20)])
+def test_analysis_many_taps_fused(gpu, N, os_, ppc):
+    """P in (16, 32]: the PMAX=32 instantiation of the fused kernel."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(N, os_, ppc)
+    x = _noise(np.random.default_rng(3), (1, 1, 40000))
+    ref = orc.polyphase_analysis(x, taps, N, os_)
+    got = pfb.polyphase_analysis(torch.from_numpy(x).to(gpu), taps, N, os_).cpu().numpy()
+    assert_pfb_close(got, ref)
+
+
+def test_analysis_generic_path(gpu):
+    """N > 256 goes through the FIR + row-FFT kernels."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(512, "8/7", 12)
+    x = _noise(np.random.default_rng(5), (1, 1, 60000))
+    ref = orc.polyphase_analysis(x, taps, 512, "8/7")
+    got = pfb.polyphase_analysis(torch.from_numpy(x).to(gpu), taps, 512, "8/7").cpu().numpy()
+    assert_pfb_close(got, ref)
+
+
+def test_analysis_padded_mid(gpu):
+    """SKA-Mid commutator PFB: 4096 channels, 100353 two-stage taps (C3, reduced length)."""
+    import torch
+    pfb = _pfb()
+    taps = _taps("mid")
+    assert len(taps) == 100353
+    x = _noise(np.random.default_rng(11), (1, 1, 1 << 20))
+    ref = orc.polyphase_analysis_padded(x, taps, 4096, "8/7")
+    got = pfb.polyphase_analysis_padded(torch.from_numpy(x).to(gpu), taps, 4096, "8/7")
+    assert_pfb_close(got.cpu().numpy(), ref)
+
+
+def test_analysis_short_input(gpu):
+    """n_dat shorter than the filter: zero output rows (polyphase_analysis.m:62)."""
+    pfb = _pfb()
+    taps = _taps("test")
+    x = _noise(np.random.default_rng(0), (1, 1, 50))
+    got = pfb.polyphase_analysis(x, taps, 8, "8/7")
+    assert got.shape == (1, 8, 0)
+
+
+# ----------------------------------------------------------------------------- synthesis
+def _synth_case(pfb, x, spans, nf, os_, deripple, taps, ov, taper, combine=1, sample_offset=1):
+    import torch
+    t_orc = orc.pfb_window(taper, nf, ov)
+    t_gpu = pfb.PFBWindow().lookup[taper](nf, ov)
+    dr = {"apply_deripple": deripple, "filter_coeff": taps}
+    ref = orc.polyphase_synthesis(x, spans, nf, os_, dr, sample_offset, ov, t_orc, None, combine)
+    got = pfb.polyphase_synthesis(torch.from_numpy(x).cuda(), spans, nf, os_, dr, sample_offset,
+                                  ov, t_gpu, None, combine)
+    return got.cpu().numpy(), ref
+
+
+@pytest.mark.parametrize("spans", [1, 0])
+@pytest.mark.parametrize("deripple", [1, 0])
+@pytest.mark.parametrize("taper", ["tukey", "no_window", "top_hat", "hann"])
+def test_synthesis_small_matches_oracle(gpu, spans, deripple, taper):
+    pfb = _pfb()
+    taps = _taps("test")
+    x = _noise(np.random.default_rng(21), (2, 8, 96 * 7 + 32 + 5))
+    got, ref = _synth_case(pfb, x, spans, 128, "8/7", deripple, taps, 16, taper)
+    assert_pfb_close(got, ref, what=f"synthesis spans={spans} dr={deripple} {taper}")
+
+
+def test_synthesis_literal_agreement_small(gpu):
+    """GPU vs the literal (statement-by-statement) transliteration."""
+    import torch
+    pfb = _pfb()
+    taps = _taps("test")
+    x = _noise(np.random.default_rng(22), (1, 8, 96 * 3 + 32))
+    t_orc = orc.pfb_window("tukey", 128, 16)
+    dr = {"apply_deripple": 1, "filter_coeff": taps}
+    ref = orc.polyphase_synthesis_literal(x, 1, 128, "8/7", dr, 1, 16, t_orc)
+    got = pfb.polyphase_synthesis(torch.from_numpy(x).cuda(), 1, 128, "8/7", dr, 1, 16,
+                                  pfb.PFBWindow().lookup["tukey"](128, 16)).cpu().numpy()
+    assert_pfb_close(got, ref)
+
+
+@pytest.mark.parametrize("combine", [2, 4])
+def test_synthesis_combine(gpu, combine):
+    pfb = _pfb()
+    taps = _taps("test")
+    x = _noise(np.random.default_rng(23 + combine), (1, 8, 96 * 4 + 32))
+    got, ref = _synth_case(pfb, x, 0, 128, "8/7", 0, taps, 16, "tukey", combine=combine)
+    assert_pfb_close(got, ref)
+
+
+def test_synthesis_sample_offset(gpu):
+    pfb = _pfb()
+    taps = _taps("test")
+    x = _noise(np.random.default_rng(24), (1, 8, 96 * 4 + 32 + 9))
+    got, ref = _synth_case(pfb, x, 1, 128, "8/7", 1, taps, 16, "tukey", sample_offset=7)
+    assert_pfb_close(got, ref)
+
+
+@pytest.mark.parametrize("N,os_,nf,ov,blocks", [
+    (256, "8/7", 256, 48, 12),
+    (256, "4/3", 256, 48, 10),
+    (4096, "8/7", 512, 128, 3),
+])
+def test_synthesis_baseline_shapes(gpu, N, os_, nf, ov, blocks):
+    pfb = _pfb()
+    taps = _taps({"8/7": "low87", "4/3": "low43"}[os_]) if N == 256 else _taps("mid")
+    keep = nf - 2 * ov
+    x = _noise(np.random.default_rng(N + blocks), (1, N, blocks * keep + 2 * ov + 3))
+    got, ref = _synth_case(pfb, x, 1, nf, os_, 1, taps, ov, "tukey")
+    assert_pfb_close(got, ref, what=f"synthesis N={N} {os_}")
+
+
+def test_synthesis_chunking_invariant(gpu):
+    """Chunked channel-IFFT/block kernels give identical output for any chunk size."""
+    import torch
+    pfb = _pfb()
+    x = torch.from_numpy(_noise(np.random.default_rng(31), (1, 256, 160 * 11 + 96))).cuda()
+    plan = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, False, None, "tukey", None, 1)
+    a = plan.execute(x)
+    plan.set_chunk_blocks(3)
+    b = plan.execute(x)
+    plan.set_chunk_blocks(1)
+    c = plan.execute(x)
+    assert torch.equal(a, b) and torch.equal(a, c)
+
+
+def test_synthesis_rejects_real_input(gpu):
+    pfb = _pfb()
+    with pytest.raises(ValueError):
+        pfb.polyphase_synthesis(np.zeros((1, 8, 400), dtype=np.float32), 1, 128, "8/7")
+
+
+def test_synthesis_invalid_args(gpu):
+    pfb = _pfb()
+    x = _noise(np.random.default_rng(0), (1, 8, 400))
+    with pytest.raises(pfb.PfbError):
+        # Nf*de/nu not integral
+        pfb.polyphase_synthesis(x, 1, 100, "8/7", None, 1, 16)
+
+
+# ----------------------------------------------------------------------------- round trip
+def test_round_trip_test_config(gpu):
+    """C1: 'test' config, complex sinusoid (bin 3, pi/4) through analysis -> synthesis."""
+    import torch
+    pfb = _pfb()
+    cfg = pfb.default_config("test")
+    taps = _taps("test")
+    n = 3 * 112 * 8 + 1000
+    x = _tone(n, 3, n_pol=2)
+    chan = pfb.polyphase_analysis(torch.from_numpy(x).cuda(), taps, 8, cfg.os_factor)
+    win = pfb.PFBWindow().lookup["tukey"](128, 16)
+    out = pfb.polyphase_synthesis(chan, 1, 128, cfg.os_factor,
+                                  {"apply_deripple": 1, "filter_coeff": taps}, 1, 16, win)
+    ref_chan = orc.polyphase_analysis(x, taps, 8, "8/7")
+    ref = orc.polyphase_synthesis(ref_chan, 1, 128, "8/7",
+                                  {"apply_deripple": 1, "filter_coeff": taps}, 1, 16,
+                                  orc.pfb_window("tukey", 128, 16))
+    assert_pfb_close(out.cpu().numpy(), ref)
+
+
+# ----------------------------------------------------------------------------- streaming
+def test_filterbank_streaming_matches_oracle(gpu):
+    pfb = _pfb()
+    taps = _taps("test")
+    cfg = dict(analysis_function="polyphase_analysis", filt_coeff=taps, channels=8,
+               os_factor="8/7")
+    fb = pfb.FilterBank(cfg)
+    ofb = orc.FilterBankOracle(taps, 8, "8/7")
+    rng = np.random.default_rng(41)
+    for n in (1000, 777, 2048, 5, 3001):
+        x = _noise(rng, (2, 1, n))
+        fb, got = fb.execute(x)
+        ref = ofb.execute(x)
+        assert got.shape == ref.shape
+        if ref.size:
+            assert_pfb_close(got, ref)
+        assert fb.buffered_samples == ofb.buffered_samples
+
+
+def test_filterbank_stream_equals_one_shot(gpu):
+    """Carry-over makes chunked Bunton analysis identical to a single call."""
+    import torch
+    pfb = _pfb()
+    taps = _taps("low87")
+    cfg = dict(analysis_function="polyphase_analysis", filt_coeff=taps, channels=256,
+               os_factor="8/7")
+    x = torch.from_numpy(_noise(np.random.default_rng(42), (1, 1, 1 << 17))).cuda()
+    fb = pfb.FilterBank(cfg)
+    parts = []
+    for a, b in ((0, 40000), (40000, 90001), (90001, 1 << 17)):
+        fb, y = fb.execute(x[:, :, a:b])
+        parts.append(y)
+    streamed = torch.cat(parts, dim=2)
+    whole = pfb.polyphase_analysis(x, taps, 256, "8/7")
+    assert torch.equal(streamed, whole[:, :, :streamed.shape[2]])
+
+
+def test_inverse_filterbank_streaming_matches_oracle(gpu):
+    pfb = _pfb()
+    taps = _taps("test")
+    cfg = dict(filt_coeff=taps, channels=8, os_factor="8/7", input_fft_length=128,
+               input_overlap=16, deripple=True, temporal_taper="tukey")
+    ifb = pfb.InverseFilterBank(cfg)
+    oifb = orc.InverseFilterBankOracle(taps, 8, "8/7", 128, 16, "tukey", deripple=True)
+    rng = np.random.default_rng(43)
+    for n in (500, 333, 1000, 20, 777):
+        x = _noise(rng, (2, 8, n))
+        ifb, got = ifb.execute(x)
+        ref = oifb.execute(x)
+        assert got.shape == ref.shape, (got.shape, ref.shape)
+        if ref.size:
+            assert_pfb_close(got, ref)
+        assert ifb.buffered_samples == oifb.buffered_samples
