@@ -44,6 +44,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--chunk-blocks", type=int, default=0)
+    ap.add_argument("--graph", type=int, default=1,
+                    help="capture one step (3 kernel launches) in a HIP graph and replay it")
+    ap.add_argument("--kernel-events", type=int, default=1,
+                    help="record HIP events around every kernel in the timed region")
     return ap.parse_args()
 
 
@@ -128,24 +132,47 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    run = step
+    if args.graph:
+        # the plans own all their device buffers after the warm-up, so the step is
+        # capturable: one graph launch replays analysis + channel IFFT + block kernel
+        graph = torch.cuda.CUDAGraph()
+        cs = torch.cuda.Stream(device=dev)
+        cs.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(cs):
+            step()
+        torch.cuda.current_stream(dev).wait_stream(cs)
+        with torch.cuda.graph(graph):
+            step()
+        torch.cuda.synchronize(dev)
+        run = graph.replay
 
+    def timed(steps, fn):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    # timed region: K steps, no instrumentation (value, ms_per_step)
+    el = timed(args.steps, run)
+    # profiled region: the same K steps with HIP events recorded around every kernel
+    # launch on the library's launch stream (per-kernel durations for the roofline;
+    # the events add inter-kernel gaps, so this region is not used for `value`)
     lib.pfb_profile_reset()
-    lib.pfb_profile_enable(1)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        y = step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
+    lib.pfb_profile_enable(args.kernel_events)
+    el_prof = timed(args.steps, step)
     lib.pfb_profile_enable(0)
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
 
     # per-kernel-class event timings (on the library's launch stream)
     import ctypes
@@ -162,9 +189,12 @@ def main():
     if rank == 0:
         samples = world * n_pol * n_dat * args.steps
         value = samples / el / 1e6
-        dom = max(kern, key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"])
-        kd = kern[dom]
-        achieved = kd["alg_bytes_per_launch"] / (kd["avg_ms"] * 1e-3) / 1e9
+        if kern:
+            dom = max(kern, key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"])
+            kd = kern[dom]
+            achieved = kd["alg_bytes_per_launch"] / (kd["avg_ms"] * 1e-3) / 1e9
+        else:
+            dom, achieved = None, 0.0
         traffic = pmc_traffic()
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -190,9 +220,11 @@ def main():
                        "n_chan": N_CHAN, "os_factor": OS_STR, "n_taps": len(taps),
                        "n_dat_per_unit": n_dat, "n_pol": n_pol, "units": world * n_pol,
                        "channelised_rows": K, "output_samples_per_unit": n_out,
-                       "parallelism": f"{world} independent units, one per GPU (no collective)"},
+                       "parallelism": f"{world} independent units, one per GPU (no collective)",
+                       "hip_graph": bool(args.graph)},
             "roofline": roof,
             "round_trip_hbm_frac": round(rt_gbs / HBM_PEAK_GBS, 4),
+            "ms_per_step_with_kernel_events": round(el_prof / args.steps * 1e3, 4),
             "kernels": kern,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -1,0 +1,51 @@
+"""Summarise rocprofv3 --pmc CSV passes per kernel (mean counter value per dispatch).
+
+HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read, so read bytes =
+2 * FETCH_SIZE * 1024 (the guide's correction); WRITE_SIZE * 1024 is exact for 16-B
+streaming stores.  Infinity-Cache hits are counted too (the counters sit on the L2's
+memory side), so this is L2<->fabric traffic, an upper bound of HBM traffic.
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def short(name):
+    for k in ("analysis_fused", "row_fft", "synth_block", "fir_generic"):
+        if k in name:
+            return name.split("(")[0].replace("void pfb::", "")
+    return None
+
+
+def load(dirs):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for d in dirs:
+        for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    k = short(row["Kernel_Name"])
+                    if k:
+                        acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+
+
+if __name__ == "__main__":
+    res = load(sys.argv[1:] if len(sys.argv) > 1 else ["."])
+    for k, cs in res.items():
+        print(f"== {k}")
+        for c in sorted(cs):
+            print(f"   {c:28s} {cs[c]:16.1f}")
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+            rd = 2 * cs["FETCH_SIZE"] * 1024
+            wr = cs["WRITE_SIZE"] * 1024
+            print(f"   -> read {rd/1e6:.1f} MB (2x FETCH_SIZE), write {wr/1e6:.1f} MB per dispatch")
+        if "SQ_LDS_BANK_CONFLICT" in cs and "SQ_LDS_IDX_ACTIVE" in cs:
+            print(f"   -> LDS bank-conflict cycles / LDS active = "
+                  f"{cs['SQ_LDS_BANK_CONFLICT']/max(cs['SQ_LDS_IDX_ACTIVE'],1):.3f}")
+        if "SQ_WAVE_CYCLES" in cs:
+            w = cs["SQ_WAVE_CYCLES"]
+            print(f"   -> wait_any {cs.get('SQ_WAIT_ANY',0)/w:.2f}  wait_inst {cs.get('SQ_WAIT_INST_ANY',0)/w:.2f}"
+                  f"  active {cs.get('SQ_ACTIVE_INST_ANY',0)/w:.2f} of wave cycles")

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -148,6 +149,7 @@ struct pfb_analysis_plan {
   int variant = 0, N = 0, nu = 1, de = 1, M = 0, P = 0, n_pol = 1, sds = 0;
   int64_t n_taps = 0;
   bool fused = false;
+  int tile_div = 1;  // PFB_ANALYSIS_TILE_DIV (experiment knob): 1 or 2
   DevBuf taps, twN, scratch;
   // streaming (FilterBank.m:13-14 input_buffer / buffered_samples)
   DevBuf carry, work, stage_in, stage_out;
@@ -173,6 +175,7 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   a.taps = p->taps.as<float>();
   a.twN = p->twN.as<float2>();
   a.scratch = nullptr;
+  a.tile_div = p->tile_div;
   if (!p->fused) {
     HIPCHK(p->scratch.ensure((size_t)p->n_pol * K * p->N * sizeof(float2)));
     a.scratch = p->scratch.as<float2>();
@@ -240,7 +243,9 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
     delete p;
     return fail(PFB_ERR_HIP, "hipSetDevice(%d) failed", d->device);
   }
-  std::vector<float> taps((size_t)p->P * p->N, 0.f);
+  if (const char* td = std::getenv("PFB_ANALYSIS_TILE_DIV")) p->tile_div = std::atoi(td) == 2 ? 2 : 1;
+  // zero rows up to the fused kernel's PMAX (32) so its tap loads are unconditional
+  std::vector<float> taps((size_t)std::max(p->P, 32) * p->N, 0.f);
   for (int64_t i = 0; i < d->n_taps; ++i) taps[(size_t)i] = (float)d->taps[i];  // cast(filt, 'single')
   hipError_t e = upload(p->taps, taps);
   if (e == hipSuccess) e = upload(p->twN, twiddles(p->N, -1));
@@ -388,7 +393,7 @@ struct pfb_synthesis_plan {
   int chunk_blocks = 0;
   bool identity_perm = true;
   bool has_cgain = false;
-  DevBuf window, src, gain, expo, twL, twN, twNf, twW, perm, cgain;
+  DevBuf window, tw4, twN, twNf, twW, perm, cgain;
   DevBuf Z, carry, work, stage_in, stage_out;
   int64_t buffered = 0;
 };
@@ -413,7 +418,9 @@ static pfb_status synthesis_run(pfb_synthesis_plan* p, const float2* in, int64_t
   if (B == 0) return PFB_OK;
   int64_t CB = p->chunk_blocks;
   if (CB <= 0) {
-    const int64_t target = (int64_t)1 << 22;  // ~32 MB of Z per chunk
+    // one chunk up to 2^26 channel-rows x channels (512 MB of Z); fewer, larger
+    // launches measured faster than MALL-sized chunks (profiles/r01 sweep)
+    const int64_t target = (int64_t)1 << 26;
     CB = std::max<int64_t>(1, target / ((int64_t)p->keep * p->N * p->n_pol));
   }
   CB = std::min<int64_t>(CB, B);
@@ -457,10 +464,8 @@ static pfb_status synthesis_run(pfb_synthesis_plan* p, const float2* in, int64_t
     a.t1_hi = p->t1_hi;
     a.scale = (float)((double)p->de / (double)p->nu / (double)p->L);
     a.window = p->window.as<float>();
-    a.src = p->src.as<int>();
-    a.gain = p->gain.as<float>();
-    a.expo = p->expo.as<int>();
-    a.twL = p->twL.as<float2>();
+    a.spans = p->spans;
+    a.tw4 = p->tw4.as<float2>();
     a.twNf = p->twNf.as<float2>();
     a.twW = p->twW.as<float2>();
     a.out_limit = out_limit;
@@ -611,7 +616,7 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
     }
   }
   std::vector<int> src((size_t)W), expo((size_t)W);
-  std::vector<float> gain((size_t)W);
+  std::vector<double> gain((size_t)W);
   for (int jp = 0; jp < W; ++jp) {
     int j, e;
     if (p->spans) {
@@ -623,18 +628,27 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
     }
     src[(size_t)jp] = (d2 + j + Nf / 2) % Nf;
     expo[(size_t)jp] = e;
-    gain[(size_t)jp] = (float)((j < W2) ? g[(size_t)(W2 - j)] : g[(size_t)(j - W2)]);
+    gain[(size_t)jp] = (j < W2) ? g[(size_t)(W2 - j)] : g[(size_t)(j - W2)];
   }
   hipError_t e = upload(p->window, window);
-  if (e == hipSuccess) e = upload(p->src, src);
-  if (e == hipSuccess) e = upload(p->gain, gain);
-  if (e == hipSuccess) e = upload(p->expo, expo);
+  // four-step twiddle x deripple gain, laid out [t0][j'] (coalesced in the block kernel)
+  std::vector<float2> tw4((size_t)N * W);
+  for (int t0 = 0; t0 < N; ++t0) {
+    for (int jp = 0; jp < W; ++jp) {
+      int64_t m = ((int64_t)t0 * expo[(size_t)jp]) % p->L;
+      if (m < 0) m += p->L;
+      if (2 * m > p->L) m -= p->L;
+      const double ang = 2.0 * M_PI * (double)m / (double)p->L;
+      const double gj = gain[(size_t)jp];
+      tw4[(size_t)t0 * W + jp] = make_float2((float)(gj * std::cos(ang)), (float)(gj * std::sin(ang)));
+    }
+  }
+  if (e == hipSuccess) e = upload(p->tw4, tw4);
   if (e == hipSuccess) e = upload(p->perm, perm);
   if (e == hipSuccess && !cgain.empty()) {
     e = upload(p->cgain, cgain);
     p->has_cgain = true;
   }
-  if (e == hipSuccess) e = upload(p->twL, twiddles(p->L, +1));
   if (e == hipSuccess) e = upload(p->twN, twiddles(N, -1));
   if (e == hipSuccess) e = upload(p->twNf, twiddles(Nf, -1));
   if (e == hipSuccess) e = upload(p->twW, twiddles(W, -1));
@@ -649,7 +663,7 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
 pfb_status pfb_synthesis_plan_destroy(pfb_synthesis_plan* p) {
   if (!p) return PFB_OK;
   (void)hipSetDevice(p->device);
-  for (DevBuf* b : {&p->window, &p->src, &p->gain, &p->expo, &p->twL, &p->twN, &p->twNf, &p->twW,
+  for (DevBuf* b : {&p->window, &p->tw4, &p->twN, &p->twNf, &p->twW,
                     &p->perm, &p->cgain, &p->Z, &p->carry, &p->work, &p->stage_in, &p->stage_out})
     b->release();
   delete p;

@@ -40,19 +40,22 @@ struct AnalysisStore {
   }
 };
 
+// Row loader of the first FFT pass.  Rows past the end are clamped to the last valid
+// row (their results are never stored), so every load is unconditional and the
+// compiler can issue them back to back.
+template <bool PERM, bool GAIN>
 struct RowLoad {
   static constexpr bool kIsLds = false;
   const float2* in;
-  int64_t r0, n_rows;
+  int64_t r0, last;
   int N;
   const int* perm;
   const float* cgain;
   __device__ __forceinline__ float2 load(int row, int i) const {
-    const int64_t r = r0 + row;
-    if (r >= n_rows) return make_float2(0.f, 0.f);
-    const int c = perm ? perm[i] : i;
+    const int64_t r = min(r0 + row, last);
+    const int c = PERM ? perm[i] : i;
     float2 v = in[r * N + c];
-    if (cgain) v = cscale(v, cgain[c]);  // taper acts on input rows (before the re-ordering)
+    if constexpr (GAIN) v = cscale(v, cgain[c]);  // taper acts on input rows (before re-ordering)
     return v;
   }
 };
@@ -79,45 +82,83 @@ struct RowStore {
 };
 
 // ======================================================================= analysis
-template <int N>
+template <int N, int PMAX, int TDIV = 1>
 struct AnaShape {
-  static constexpr int T = 4096 / N;        // output rows per workgroup
+  static constexpr int T = 4096 / N / TDIV; // output rows per workgroup
   static constexpr int RS = lds_row(N);     // padded LDS row (float2)
   static constexpr int KSTEP = NT / N;      // rows covered by one thread sweep
   static constexpr int KPT = T / KSTEP;     // rows per thread (= 16)
+  // input span S = M (T-1) + P N <= N (T-1) + PMAX N samples, staged as float4 pairs
+  static constexpr int SMAX = N * (T - 1) + PMAX * N;
+  static constexpr int CH = (SMAX / 2 + NT - 1) / NT;  // float4 chunks per thread
 };
 
-template <int N, int PMAX, int VARIANT>
+// XCD-aware tile order: workgroups b and b+8 share an XCD (and its L2); give them
+// consecutive tiles so the halo of one tile is an L2 hit for its neighbour.
+// Bijective for any grid size (cdna_hip_programming.md, "XCD swizzle must be bijective").
+__device__ __forceinline__ int xcd_tile(int b, int nwg) {
+  const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+// Stage x[base, base + S) into LDS (zero outside [0, n_dat)).  Interior tiles issue
+// all of their 16-byte loads back to back before the first LDS write.
+template <int CH>
+__device__ __forceinline__ void stage_span(float2* smem, const float2* __restrict__ x,
+                                           int64_t base, int S, int64_t n_dat, int tid) {
+  const int S2 = (S + 1) >> 1;
+  const bool interior = base >= 0 && base + 2 * (int64_t)S2 <= n_dat &&
+                        ((reinterpret_cast<uintptr_t>(x + base) & 15) == 0);
+  if (interior) {
+    const float4* __restrict__ src = reinterpret_cast<const float4*>(x + base);
+    float4 v[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) v[i] = src[min(tid + i * NT, S2 - 1)];
+    // unconditional (clamped) stores: a guarded store lets the compiler sink each load
+    // into its branch and wait for it there, serialising the HBM latency
+#pragma unroll
+    for (int i = 0; i < CH; ++i) reinterpret_cast<float4*>(smem)[min(tid + i * NT, S2 - 1)] = v[i];
+  } else {
+    for (int s = tid; s < S; s += NT) {
+      const int64_t g = base + s;
+      smem[s] = (g >= 0 && g < n_dat) ? x[g] : make_float2(0.f, 0.f);
+    }
+  }
+}
+
+// PMAX = compile-time tap phases; EXACT means P == PMAX (no clamping needed).
+template <int N, int PMAX, int VARIANT, int TDIV, bool EXACT>
 __global__ __launch_bounds__(NT) void analysis_fused_kernel(AnalysisArgs a) {
   static_assert(NT % N == 0, "fused analysis needs N | 256");
-  using S_ = AnaShape<N>;
+  using S_ = AnaShape<N, PMAX, TDIV>;
   constexpr int T = S_::T;
   extern __shared__ __attribute__((aligned(16))) float2 smem[];
   const int tid = threadIdx.x;
   const int pol = blockIdx.y;
-  const int64_t k0 = (int64_t)blockIdx.x * T;
+  const int64_t k0 = (int64_t)xcd_tile(blockIdx.x, gridDim.x) * T;
   const int M = a.M, P = a.P;
   const int PN = P * N;
   const int S = M * (T - 1) + PN;
   const float2* __restrict__ x = a.in + pol * a.in_pol_stride;
 
-  // 1. stage the input span of the T rows (Bunton: x[k0 M + s]; padded: x[k0 M - PN + s],
-  //    zero history before t = 0, polyphase_analysis_padded.m:101-102)
-  const int64_t base = (VARIANT == kBunton) ? k0 * M : k0 * M - PN;
-  for (int s = tid; s < S; s += NT) {
-    const int64_t g = base + s;
-    smem[s] = (g >= 0 && g < a.n_dat) ? x[g] : make_float2(0.f, 0.f);
-  }
-  // 2. this thread's polyphase arm n: taps f[m N + n] in registers
+  // 1. this thread's polyphase arm n: taps f[m N + n] in registers (taps are padded
+  //    with zero rows to PMAX on the device, so the loads are unconditional)
   const int n = tid % N;
   const int kk0 = tid / N;
   float tr[PMAX];
 #pragma unroll
-  for (int m = 0; m < PMAX; ++m) tr[m] = (m < P) ? a.taps[m * N + n] : 0.f;
+  for (int m = 0; m < PMAX; ++m) tr[m] = a.taps[m * N + n];
+  // 2. stage the input span of the T rows (Bunton: x[k0 M + s]; padded: x[k0 M - PN + s],
+  //    zero history before t = 0, polyphase_analysis_padded.m:101-102)
+  const int64_t base = (VARIANT == kBunton) ? k0 * M : k0 * M - PN;
+  stage_span<S_::CH>(smem, x, base, S, a.n_dat, tid);
   __syncthreads();
 
   // 3. FIR: Bunton u_k[n] = sum_m f[mN+n] x[kM + mN + n]        (polyphase_analysis.m:105-115)
   //         padded y_q[n] = sum_p f[pN+n] x[qM - 1 - pN - n]      (polyphase_analysis_padded.m:118-126)
+  //    Branch-free: taps are zero for m >= P and the LDS read index is clamped to the
+  //    row's last phase (a sample of the row's own window, so 0 * x is exact even for
+  //    non-finite x); a guarded read would serialise every LDS access.
   float2 u[S_::KPT];
 #pragma unroll
   for (int e = 0; e < S_::KPT; ++e) {
@@ -127,26 +168,27 @@ __global__ __launch_bounds__(NT) void analysis_fused_kernel(AnalysisArgs a) {
       const float2* p = smem + k * M + n;
 #pragma unroll
       for (int m = 0; m < PMAX; ++m) {
-        if (m < P) {
-          const float2 v = p[m * N];
-          ax = fmaf(tr[m], v.x, ax);
-          ay = fmaf(tr[m], v.y, ay);
-        }
+        const int mm = EXACT ? m : min(m, P - 1);
+        const float2 v = p[mm * N];
+        ax = fmaf(tr[m], v.x, ax);
+        ay = fmaf(tr[m], v.y, ay);
       }
     } else {
       const float2* p = smem + k * M + PN - 1 - n;
 #pragma unroll
       for (int m = 0; m < PMAX; ++m) {
-        if (m < P) {
-          const float2 v = p[-m * N];
-          ax = fmaf(tr[m], v.x, ax);
-          ay = fmaf(tr[m], v.y, ay);
-        }
+        const int mm = EXACT ? m : min(m, P - 1);
+        const float2 v = p[-mm * N];
+        ax = fmaf(tr[m], v.x, ax);
+        ay = fmaf(tr[m], v.y, ay);
       }
     }
     u[e] = make_float2(ax, ay);
   }
+  // twiddle table -> LDS, behind the FFT rows (the staged span is dead after the FIR)
+  const float2 twv = a.twN[tid & (N - 1)];
   __syncthreads();
+  if (tid < N) smem[T * S_::RS + tid] = twv;
 
   // 4. circular shift folded into the LDS write address
   //    Bunton: v[(n + r) mod N] = u[n], r = (M k) mod N               (polyphase_analysis.m:102-105)
@@ -172,7 +214,7 @@ __global__ __launch_bounds__(NT) void analysis_fused_kernel(AnalysisArgs a) {
   // 5. N-point DFT of every row; Bunton N*fft (forward), padded N^2*ifft (inverse dir.)
   AnalysisStore st{a.out + pol * a.out_pol_stride, a.K, k0, N, a.sds, VARIANT == kPadded,
                    (float)N};
-  block_fft<N, (VARIANT == kBunton) ? -1 : +1, T, NT>(rows, st, rows, a.twN, tid);
+  block_fft<N, (VARIANT == kBunton) ? -1 : +1, T, NT>(rows, st, rows, smem + T * S_::RS, tid);
 }
 
 template <int VARIANT>
@@ -228,16 +270,25 @@ struct RowShape {
   static constexpr int RS = lds_row(N);
 };
 
-template <int N, int DIR>
+template <int N, int DIR, bool PERM, bool GAIN>
 __global__ __launch_bounds__(NT) void row_fft_kernel(RowFftArgs a) {
   constexpr int ROWS = RowShape<N>::ROWS;
   extern __shared__ __attribute__((aligned(16))) float2 smem[];
   const int pol = blockIdx.y;
   const int64_t r0 = (int64_t)blockIdx.x * ROWS;
-  RowLoad ld{a.in + pol * a.in_pol_stride, r0, a.n_rows, N, a.perm, a.cgain};
+  RowLoad<PERM, GAIN> ld{a.in + pol * a.in_pol_stride, r0, a.n_rows - 1, N, a.perm, a.cgain};
   RowStore st{a.out + pol * a.out_pol_stride, r0, a.n_rows, N, a.sds, a.remap, a.scale};
   LdsRows rows(smem, RowShape<N>::RS);
-  block_fft<N, DIR, ROWS, NT>(ld, st, rows, a.tw, threadIdx.x);
+  // twiddle table -> LDS behind the rows (ordered before pass 2 by its barrier)
+  float2* tw = smem + ROWS * RowShape<N>::RS;
+  constexpr int TPT = (N + NT - 1) / NT;
+  float2 twv[TPT];
+#pragma unroll
+  for (int i = 0; i < TPT; ++i) twv[i] = a.tw[(threadIdx.x + i * NT) & (N - 1)];
+#pragma unroll
+  for (int i = 0; i < TPT; ++i)
+    if (threadIdx.x + i * NT < N) tw[threadIdx.x + i * NT] = twv[i];
+  block_fft<N, DIR, ROWS, NT>(ld, st, rows, tw, threadIdx.x);
 }
 
 // ======================================================================= synthesis block
@@ -246,7 +297,8 @@ struct SynthShape {
   static constexpr int RSF = lds_row(NF) | 1;  // odd row stride: conflict-free column writes
   static constexpr int RSW = lds_row(W) | 1;
   static constexpr int RSMAX = RSF > RSW ? RSF : RSW;
-  static constexpr size_t lds_bytes = (size_t)TG * RSMAX * sizeof(float2);
+  static constexpr int TWOFF = TG * RSMAX;  // twiddle tables (NF + W) + window behind the rows
+  static constexpr size_t lds_bytes = (size_t)(TWOFF + NF + W) * sizeof(float2) + NF * sizeof(float);
 };
 
 template <int NF, int W, int TG>
@@ -261,20 +313,53 @@ __global__ __launch_bounds__(NT) void synth_block_kernel(SynthBlockArgs a) {
   const float2* __restrict__ Z = a.Z + pol * a.z_pol_stride + (int64_t)bl * a.keep * N + t0;
 
   // 1. temporal taper + transpose: row i <- Z[tau][t0 + i]   (polyphase_synthesis.m:176-185)
-  for (int idx = tid; idx < TG * NF; idx += NT) {
-    const int i = idx % TG;
+  static_assert((TG * NF) % NT == 0, "tile must be a multiple of the workgroup");
+  constexpr int LPT = TG * NF / NT;
+  float2* twF = smem + SS::TWOFF;        // Nf twiddles, then W twiddles, then the window
+  float2* twWl = twF + NF;
+  float* win = reinterpret_cast<float*>(twWl + W);
+  float2 zv[LPT];
+#pragma unroll
+  for (int e = 0; e < LPT; ++e) {
+    const int idx = tid + e * NT;
+    zv[e] = Z[(int64_t)(idx / TG) * N + (idx % TG)];
+  }
+  // twiddle tables of both transforms and the temporal window -> LDS
+  constexpr int TF = (NF + W + NT - 1) / NT;
+  constexpr int TW_ = (NF + NT - 1) / NT;
+  float2 twv[TF];
+  float wv[TW_];
+#pragma unroll
+  for (int i = 0; i < TF; ++i) {
+    const int j = min(tid + i * NT, NF + W - 1);
+    twv[i] = (j < NF) ? a.twNf[j] : a.twW[j - NF];
+  }
+#pragma unroll
+  for (int i = 0; i < TW_; ++i) wv[i] = a.window[min(tid + i * NT, NF - 1)];
+#pragma unroll
+  for (int i = 0; i < TF; ++i)
+    if (tid + i * NT < NF + W) twF[tid + i * NT] = twv[i];
+#pragma unroll
+  for (int i = 0; i < TW_; ++i)
+    if (tid + i * NT < NF) win[tid + i * NT] = wv[i];
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < LPT; ++e) {
+    const int idx = tid + e * NT;
     const int tau = idx / TG;
-    const float2 v = Z[(int64_t)tau * N + i];
-    smem[i * SS::RSF + lpad(tau)] = cscale(v, a.window[tau]);
+    smem[(idx % TG) * SS::RSF + lpad(tau)] = cscale(zv[e], win[tau]);
   }
   __syncthreads();
   // 2. Nf-point forward FFT over time for every t0 row
   LdsRows rowsF(smem, SS::RSF);
-  block_fft<NF, -1, TG, NT>(rowsF, rowsF, rowsF, a.twNf, tid);
+  block_fft<NF, -1, TG, NT>(rowsF, rowsF, rowsF, twF, tid);
   __syncthreads();
 
   // 3. keep W bins (fftshift + discard, :188,240), deripple gain (:242-251), four-step
-  //    twiddle e^{+2 pi i t0 expo / L} (carries the spans-Nyquist W/2 stitch shift)
+  //    twiddle e^{+2 pi i t0 expo / L} (carries the spans-Nyquist W/2 stitch shift);
+  //    gain x twiddle come from one [t0][j'] table so the lookup is coalesced
+  //    kept bin of slot j': spans Nyquist -> signed frequency j' (j' < W/2) or
+  //    j' - W (j' >= W/2); critical -> fftshift(...)(d2 + j')
   constexpr int SEL = (TG * W + NT - 1) / NT;
   float2 sv[SEL];
 #pragma unroll
@@ -283,11 +368,10 @@ __global__ __launch_bounds__(NT) void synth_block_kernel(SynthBlockArgs a) {
     if (idx < TG * W) {
       const int i = idx / W;
       const int jp = idx - i * W;
-      int m = (t0 + i) * a.expo[jp];
-      m %= a.L;
-      if (m < 0) m += a.L;
-      const float2 s = rowsF.load(i, a.src[jp]);
-      sv[e] = cmul(cscale(s, a.gain[jp]), a.twL[m]);
+      int src;
+      if (a.spans) src = (jp < W / 2) ? jp : jp + NF - W;
+      else src = (jp < W / 2) ? jp + NF - W / 2 : jp - W / 2;
+      sv[e] = cmul(rowsF.load(i, src), a.tw4[(int64_t)(t0 + i) * W + jp]);  // coalesced
     }
   }
   __syncthreads();
@@ -302,7 +386,7 @@ __global__ __launch_bounds__(NT) void synth_block_kernel(SynthBlockArgs a) {
   }
   __syncthreads();
   // 4. W-point inverse FFT per t0 row
-  block_fft<W, +1, TG, NT>(rowsW, rowsW, rowsW, a.twW, tid);
+  block_fft<W, +1, TG, NT>(rowsW, rowsW, rowsW, twWl, tid);
   __syncthreads();
 
   // 5. overlap-discard (:302) and scale 1/L * de/nu (:285), y[t0 + N t1]
@@ -328,13 +412,13 @@ static hipError_t set_lds(K kernel, size_t bytes) {
   return hipSuccess;
 }
 
-template <int N, int PMAX, int VARIANT>
+template <int N, int PMAX, int VARIANT, int TDIV, bool EXACT = false>
 static hipError_t launch_fused(const AnalysisArgs& a, hipStream_t s) {
-  using S_ = AnaShape<N>;
+  using S_ = AnaShape<N, PMAX, TDIV>;
   const size_t span = (size_t)a.M * (S_::T - 1) + (size_t)a.P * N;
-  const size_t rows = (size_t)S_::T * S_::RS;
-  const size_t bytes = (span > rows ? span : rows) * sizeof(float2);
-  auto kern = analysis_fused_kernel<N, PMAX, VARIANT>;
+  const size_t rows = (size_t)S_::T * S_::RS + N;  // FFT rows + twiddle table
+  const size_t bytes = ((span + 1 > rows) ? span + 1 : rows) * sizeof(float2);
+  auto kern = analysis_fused_kernel<N, PMAX, VARIANT, TDIV, EXACT>;
   hipError_t e = set_lds(kern, bytes);
   if (e != hipSuccess) return e;
   dim3 grid((unsigned)((a.K + S_::T - 1) / S_::T), (unsigned)a.n_pol);
@@ -344,8 +428,16 @@ static hipError_t launch_fused(const AnalysisArgs& a, hipStream_t s) {
 
 template <int N, int VARIANT>
 static hipError_t launch_fused_p(const AnalysisArgs& a, hipStream_t s) {
-  if (a.P <= 16) return launch_fused<N, 16, VARIANT>(a, s);
-  return launch_fused<N, 32, VARIANT>(a, s);
+  // exact instantiations for the configured tap counts (SKA-Low 13 and 12 phases,
+  // the 'test' config 11); other P use the clamped PMAX 16/32 kernels
+  if (a.P == 13) {
+    if (a.tile_div == 2) return launch_fused<N, 13, VARIANT, 2, true>(a, s);
+    return launch_fused<N, 13, VARIANT, 1, true>(a, s);
+  }
+  if (a.P == 12) return launch_fused<N, 12, VARIANT, 1, true>(a, s);
+  if (a.P == 11) return launch_fused<N, 11, VARIANT, 1, true>(a, s);
+  if (a.P <= 16) return launch_fused<N, 16, VARIANT, 1>(a, s);
+  return launch_fused<N, 32, VARIANT, 1>(a, s);
 }
 
 template <int N>
@@ -354,16 +446,26 @@ static hipError_t launch_fused_v(const AnalysisArgs& a, hipStream_t s) {
   return launch_fused_p<N, kPadded>(a, s);
 }
 
-template <int N, int DIR>
-static hipError_t launch_row_fft(const RowFftArgs& r, int n_pol, hipStream_t s) {
+template <int N, int DIR, bool PERM, bool GAIN>
+static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s) {
   constexpr int ROWS = RowShape<N>::ROWS;
-  const size_t bytes = (size_t)ROWS * RowShape<N>::RS * sizeof(float2);
-  auto kern = row_fft_kernel<N, DIR>;
+  const size_t bytes = ((size_t)ROWS * RowShape<N>::RS + N) * sizeof(float2);
+  auto kern = row_fft_kernel<N, DIR, PERM, GAIN>;
   hipError_t e = set_lds(kern, bytes);
   if (e != hipSuccess) return e;
   dim3 grid((unsigned)((r.n_rows + ROWS - 1) / ROWS), (unsigned)n_pol);
   hipLaunchKernelGGL(kern, grid, dim3(NT), bytes, s, r);
   return hipGetLastError();
+}
+
+template <int N, int DIR>
+static hipError_t launch_row_fft(const RowFftArgs& r, int n_pol, hipStream_t s) {
+  if constexpr (DIR > 0) {
+    if (r.perm && r.cgain) return launch_row_fft_t<N, DIR, true, true>(r, n_pol, s);
+    if (r.perm) return launch_row_fft_t<N, DIR, true, false>(r, n_pol, s);
+    if (r.cgain) return launch_row_fft_t<N, DIR, false, true>(r, n_pol, s);
+  }
+  return launch_row_fft_t<N, DIR, false, false>(r, n_pol, s);
 }
 
 template <int DIR>

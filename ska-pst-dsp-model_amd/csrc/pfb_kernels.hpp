@@ -23,6 +23,7 @@ struct AnalysisArgs {
   const float* taps;       // P*N padded taps (device)
   const float2* twN;       // e^{-2 pi i m / N}, m < N (device)
   float2* scratch;         // generic path: [pol][K][N] (device) or null
+  int tile_div;            // fused kernel: rows per workgroup = 4096 / N / tile_div (1 or 2)
 };
 
 // Synthesis stage 1: per channelised time row, N-point inverse DFT across channels
@@ -54,10 +55,8 @@ struct SynthBlockArgs {
   int N, Nf, W, keep, L, Lov, Lkeep, t1_lo, t1_hi;
   float scale;
   const float* window;     // Nf temporal window (device)
-  const int* src;          // W: source FFT bin
-  const float* gain;       // W: deripple gain
-  const int* expo;         // W: signed twiddle exponent
-  const float2* twL;       // e^{+2 pi i m / L}, m < L
+  int spans;               // 1: spans Nyquist (signed-frequency bins), 0: critical
+  const float2* tw4;       // [t0][j'] = gain[j'] e^{+2 pi i t0 expo[j'] / L} (N x W)
   const float2* twNf;      // e^{-2 pi i m / Nf}
   const float2* twW;       // e^{-2 pi i m / W}
   int64_t out_limit;       // samples per pol actually written (InverseFilterBank trim)
