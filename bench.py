@@ -67,7 +67,7 @@ def cpu_baseline(taps, budget_s: float):
         orc.polyphase_synthesis(chan, 1, NF, OS_STR, dr, 1, OV, win, dtype=np.complex64)
         reps += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or reps >= 64:
+        if el >= budget_s or reps >= 4096:
             break
     return {
         "value": reps * n / el / 1e6,

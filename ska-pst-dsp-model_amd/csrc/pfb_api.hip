@@ -149,7 +149,7 @@ struct pfb_analysis_plan {
   int variant = 0, N = 0, nu = 1, de = 1, M = 0, P = 0, n_pol = 1, sds = 0;
   int64_t n_taps = 0;
   bool fused = false;
-  int tile_div = 1;  // PFB_ANALYSIS_TILE_DIV (experiment knob): 1 or 2
+  int strips = 0;  // PFB_ANALYSIS_STRIPS (experiment knob): persistent workgroups per pol
   DevBuf taps, twN, scratch;
   // streaming (FilterBank.m:13-14 input_buffer / buffered_samples)
   DevBuf carry, work, stage_in, stage_out;
@@ -175,7 +175,7 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   a.taps = p->taps.as<float>();
   a.twN = p->twN.as<float2>();
   a.scratch = nullptr;
-  a.tile_div = p->tile_div;
+  a.strips = p->strips;
   if (!p->fused) {
     HIPCHK(p->scratch.ensure((size_t)p->n_pol * K * p->N * sizeof(float2)));
     a.scratch = p->scratch.as<float2>();
@@ -243,7 +243,7 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
     delete p;
     return fail(PFB_ERR_HIP, "hipSetDevice(%d) failed", d->device);
   }
-  if (const char* td = std::getenv("PFB_ANALYSIS_TILE_DIV")) p->tile_div = std::atoi(td) == 2 ? 2 : 1;
+  if (const char* v = std::getenv("PFB_ANALYSIS_STRIPS")) p->strips = std::max(0, std::atoi(v));
   // zero rows up to the fused kernel's PMAX (32) so its tap loads are unconditional
   std::vector<float> taps((size_t)std::max(p->P, 32) * p->N, 0.f);
   for (int64_t i = 0; i < d->n_taps; ++i) taps[(size_t)i] = (float)d->taps[i];  // cast(filt, 'single')
@@ -391,6 +391,8 @@ struct pfb_synthesis_plan {
   int W = 0, keep = 0, L = 0, Lov = 0, Lkeep = 0, t1_lo = 0, t1_hi = 0;
   bool deripple = false;
   int chunk_blocks = 0;
+  int timing_mask = 0;  // PFB_TIMING_MASK (timing experiments; results invalid when set)
+  int ranges = -1;  // PFB_SYNTH_RANGES: 0 one workgroup per block, -1 persistent auto, >0 persistent
   bool identity_perm = true;
   bool has_cgain = false;
   DevBuf window, tw4, twN, twNf, twW, perm, cgain;
@@ -469,6 +471,8 @@ static pfb_status synthesis_run(pfb_synthesis_plan* p, const float2* in, int64_t
     a.twNf = p->twNf.as<float2>();
     a.twW = p->twW.as<float2>();
     a.out_limit = out_limit;
+    a.ranges = p->ranges;
+    a.timing_mask = p->timing_mask;
     {
       ProfScope ps(2, (double)p->n_pol * (nb * p->keep * p->N * 8.0 + nb * p->Lkeep * 8.0), s);
       HIPCHK(pfb::launch_synth_block(a, s));
@@ -512,6 +516,8 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
 
   auto* p = new pfb_synthesis_plan();
   p->device = d->device;
+  if (const char* v = std::getenv("PFB_SYNTH_RANGES")) p->ranges = std::max(-1, std::atoi(v));
+  if (const char* v = std::getenv("PFB_TIMING_MASK")) p->timing_mask = std::atoi(v);
   p->N = N;
   p->nu = nu;
   p->de = de;
@@ -631,7 +637,7 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
     gain[(size_t)jp] = (j < W2) ? g[(size_t)(W2 - j)] : g[(size_t)(j - W2)];
   }
   hipError_t e = upload(p->window, window);
-  // four-step twiddle x deripple gain, laid out [t0][j'] (coalesced in the block kernel)
+  // four-step twiddle x deripple gain, laid out [j'][t0] (coalesced in the block kernel)
   std::vector<float2> tw4((size_t)N * W);
   for (int t0 = 0; t0 < N; ++t0) {
     for (int jp = 0; jp < W; ++jp) {
@@ -640,7 +646,7 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
       if (2 * m > p->L) m -= p->L;
       const double ang = 2.0 * M_PI * (double)m / (double)p->L;
       const double gj = gain[(size_t)jp];
-      tw4[(size_t)t0 * W + jp] = make_float2((float)(gj * std::cos(ang)), (float)(gj * std::sin(ang)));
+      tw4[(size_t)jp * N + t0] = make_float2((float)(gj * std::cos(ang)), (float)(gj * std::sin(ang)));
     }
   }
   if (e == hipSuccess) e = upload(p->tw4, tw4);

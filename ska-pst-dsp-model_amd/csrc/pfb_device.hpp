@@ -78,20 +78,33 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// generic complex helpers used by the small DFTs (overloaded for other complex types,
+// e.g. the two-transform cpx2 of pfb_pair.hpp)
+__device__ __forceinline__ float2 czero(float2) { return make_float2(0.f, 0.f); }
+__device__ __forceinline__ float2 cneg(float2 a) { return make_float2(-a.x, -a.y); }
+// c * a + b for real c
+__device__ __forceinline__ float2 cfmar(float c, float2 a, float2 b) {
+  return make_float2(fmaf(c, a.x, b.x), fmaf(c, a.y, b.y));
+}
+// a * (c + i s)
+__device__ __forceinline__ float2 ctwc(float2 a, float c, float s) {
+  return make_float2(fmaf(a.x, c, -a.y * s), fmaf(a.x, s, a.y * c));
+}
+
 // multiply by the compile-time twiddle e^{DIR * 2 pi i M / R}
-template <int M, int R, int DIR>
-__device__ __forceinline__ float2 ctw(float2 a) {
+template <int M, int R, int DIR, class C>
+__device__ __forceinline__ C ctw(C a) {
   if constexpr ((M % R) == 0) {
     return a;
   } else if constexpr ((4 * M) % R == 0) {
     constexpr int q = ((4 * M) / R) % 4;  // multiples of pi/2
-    if constexpr (q == 2) return make_float2(-a.x, -a.y);
+    if constexpr (q == 2) return cneg(a);
     else if constexpr (q == 1) return crot90<DIR>(a);
     else return crot90<-DIR>(a);
   } else {
     constexpr float c = (float)cos2pi(M, R);
     constexpr float s = (float)(DIR * sin2pi(M, R));
-    return make_float2(fmaf(a.x, c, -a.y * s), fmaf(a.x, s, a.y * c));
+    return ctwc(a, c, s);
   }
 }
 
@@ -107,30 +120,30 @@ constexpr int first_factor(int R) {
 
 // In-place DFT of R points held in registers, natural order in and out.
 // DIR = -1: X[k] = sum x[n] e^{-2 pi i n k / R}; DIR = +1: unnormalised inverse.
-template <int R, int DIR>
-__device__ __forceinline__ void sdft(float2* v) {
+// C is float2 (one transform) or any complex type with the helpers above.
+template <int R, int DIR, class C>
+__device__ __forceinline__ void sdft(C* v) {
   if constexpr (R == 1) {
     return;
   } else if constexpr (R == 2) {
-    float2 a = v[0];
+    C a = v[0];
     v[0] = cadd(a, v[1]);
     v[1] = csub(a, v[1]);
   } else if constexpr (R == 3) {
     constexpr float c = -0.5f;
     constexpr float s = (float)(DIR * 0.86602540378443864676372317075294);
-    float2 t = cadd(v[1], v[2]);
-    float2 d = csub(v[1], v[2]);
-    float2 m = make_float2(fmaf(c, t.x, v[0].x), fmaf(c, t.y, v[0].y));
-    // d * i s
-    float2 ids = make_float2(-s * d.y, s * d.x);
+    C t = cadd(v[1], v[2]);
+    C d = csub(v[1], v[2]);
+    C m = cfmar(c, t, v[0]);
+    C ids = crot90<+1>(cscale(d, s));  // i s d
     v[0] = cadd(v[0], t);
     v[1] = cadd(m, ids);
     v[2] = csub(m, ids);
   } else if constexpr (R == 4) {
-    float2 t0 = cadd(v[0], v[2]);
-    float2 t1 = csub(v[0], v[2]);
-    float2 t2 = cadd(v[1], v[3]);
-    float2 t3 = crot90<DIR>(csub(v[1], v[3]));
+    C t0 = cadd(v[0], v[2]);
+    C t1 = csub(v[0], v[2]);
+    C t2 = cadd(v[1], v[3]);
+    C t3 = crot90<DIR>(csub(v[1], v[3]));
     v[0] = cadd(t0, t2);
     v[2] = csub(t0, t2);
     v[1] = cadd(t1, t3);
@@ -138,30 +151,28 @@ __device__ __forceinline__ void sdft(float2* v) {
   } else if constexpr (R == 5 || R == 7) {
     // direct symmetric form: pairs (n, R-n)
     constexpr int H = (R - 1) / 2;
-    float2 sp[H], sm[H];
+    C sp[H], sm[H];
     static_for<0, H>([&](auto n) {
       sp[n] = cadd(v[n + 1], v[R - 1 - n]);
       sm[n] = csub(v[n + 1], v[R - 1 - n]);
     });
-    float2 out[R];
-    float2 x0 = v[0];
-    float2 dc = x0;
+    C out[R];
+    C x0 = v[0];
+    C dc = x0;
     static_for<0, H>([&](auto n) { dc = cadd(dc, sp[n]); });
     out[0] = dc;
     static_for<1, H + 1>([&](auto k) {
-      float2 re = x0;  // real-cos part
-      float2 im = make_float2(0.f, 0.f);
+      C re = x0;  // real-cos part
+      C im = czero(x0);
       static_for<0, H>([&](auto n) {
         constexpr int nk = (decltype(n)::value + 1) * decltype(k)::value;
         constexpr float c = (float)cos2pi(nk, R);
         constexpr float s = (float)sin2pi(nk, R);
-        re.x = fmaf(c, sp[n].x, re.x);
-        re.y = fmaf(c, sp[n].y, re.y);
-        im.x = fmaf(s, sm[n].x, im.x);
-        im.y = fmaf(s, sm[n].y, im.y);
+        re = cfmar(c, sp[n], re);
+        im = cfmar(s, sm[n], im);
       });
       // X[k] = re + DIR * i * im ; X[R-k] = re - DIR * i * im
-      float2 iim = make_float2(-im.y, im.x);  // i * im
+      C iim = crot90<+1>(im);  // i * im
       if constexpr (DIR < 0) {
         out[k] = csub(re, iim);
         out[R - k] = cadd(re, iim);
@@ -175,7 +186,7 @@ __device__ __forceinline__ void sdft(float2* v) {
     constexpr int A = first_factor(R);
     constexpr int B = R / A;
     static_assert(A * B == R && A > 1 && B > 1, "unsupported radix");
-    float2 y[A][B];
+    C y[A][B];
     static_for<0, A>([&](auto n1) {
       static_for<0, B>([&](auto n2) { y[n1][n2] = v[A * n2 + n1]; });
       sdft<B, DIR>(y[n1]);
@@ -185,7 +196,7 @@ __device__ __forceinline__ void sdft(float2* v) {
       });
     });
     static_for<0, B>([&](auto k1) {
-      float2 z[A];
+      C z[A];
       static_for<0, A>([&](auto n1) { z[n1] = y[n1][k1]; });
       sdft<A, DIR>(z);
       static_for<0, A>([&](auto k2) { v[k1 + B * k2] = z[k2]; });
@@ -309,5 +320,17 @@ __device__ __forceinline__ void block_fft(const First& first, const Last& last, 
                                           const float2* tw, int tid) {
   run_fft<N, DIR, ROWS, NT>(first, last, lds, tw, tid, typename FFTPlan<N>::type{});
 }
+
+
+// Coordinates of the first pass of FFTPlan<N>.
+template <int N, int ROWS, int NTH>
+struct FirstPassOf {
+  template <int R0, int... Rest>
+  static constexpr int radix(Radices<R0, Rest...>) { return R0; }
+  static constexpr int R = radix(typename FFTPlan<N>::type{});
+  static constexpr int NB = N / R;
+  static constexpr int TOT = ROWS * NB;
+  static constexpr int PER = (TOT + NTH - 1) / NTH;
+};
 
 }  // namespace pfb

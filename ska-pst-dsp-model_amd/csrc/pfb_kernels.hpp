@@ -23,7 +23,7 @@ struct AnalysisArgs {
   const float* taps;       // P*N padded taps (device)
   const float2* twN;       // e^{-2 pi i m / N}, m < N (device)
   float2* scratch;         // generic path: [pol][K][N] (device) or null
-  int tile_div;            // fused kernel: rows per workgroup = 4096 / N / tile_div (1 or 2)
+  int strips;              // fused kernel: persistent workgroups per pol (0 = auto)
 };
 
 // Synthesis stage 1: per channelised time row, N-point inverse DFT across channels
@@ -56,10 +56,13 @@ struct SynthBlockArgs {
   float scale;
   const float* window;     // Nf temporal window (device)
   int spans;               // 1: spans Nyquist (signed-frequency bins), 0: critical
-  const float2* tw4;       // [t0][j'] = gain[j'] e^{+2 pi i t0 expo[j'] / L} (N x W)
+  const float2* tw4;       // [j'][t0] = gain[j'] e^{+2 pi i t0 expo[j'] / L} (W x N)
   const float2* twNf;      // e^{-2 pi i m / Nf}
   const float2* twW;       // e^{-2 pi i m / W}
   int64_t out_limit;       // samples per pol actually written (InverseFilterBank trim)
+  int ranges;              // 0: one workgroup per block; -1 persistent auto; >0 persistent ranges
+  int timing_mask;         // timing experiments only (PFB_TIMING_MASK): bit0 drop Z loads,
+                           // bit1 drop output stores, bit2 drop tw4 loads (results invalid)
 };
 
 bool analysis_supported(int N, int P, int variant, bool* fused);
