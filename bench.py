@@ -80,7 +80,8 @@ def cpu_baseline(taps, budget_s: float):
 
 
 def pmc_traffic():
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary, if any."""
+    """HBM bytes per launch per kernel class from the committed PMC summary
+    (scripts/pmc_summary.py --json, FETCH_SIZE/WRITE_SIZE passes), if any."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
@@ -198,7 +199,7 @@ def main():
         traffic = pmc_traffic()
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": (traffic or {}).get(dom)}
+                "traffic": ((traffic or {}).get(dom) or {}).get("bytes")}
         # round trip as a whole, at B_alg = 16 (1 + nu/de) bytes per input sample
         b_alg = 16.0 * (1.0 + 8.0 / 7.0)
         rt_gbs = value * 1e6 * b_alg / 1e9 / world

@@ -32,8 +32,32 @@ def load(dirs):
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
+BENCH_NAME = {"analysis_fused": "analysis_fused", "fir_generic": "analysis_fir",
+              "row_fft": "synth_chan_ifft", "synth_block": "synth_block"}
+
+
+def traffic_json(res):
+    """Per bench kernel class: HBM bytes per launch (2 x FETCH_SIZE KiB + WRITE_SIZE KiB)."""
+    out = {}
+    for k, cs in res.items():
+        if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
+            continue
+        name = next((v for key, v in BENCH_NAME.items() if key in k), k)
+        rd = 2 * cs["FETCH_SIZE"] * 1024
+        wr = cs["WRITE_SIZE"] * 1024
+        out[name] = {"kernel": k, "read_bytes": rd, "write_bytes": wr, "bytes": rd + wr}
+    return out
+
+
 if __name__ == "__main__":
-    res = load(sys.argv[1:] if len(sys.argv) > 1 else ["."])
+    args = sys.argv[1:]
+    js = None
+    if args and args[0] == "--json":
+        js, args = args[1], args[2:]
+    res = load(args if args else ["."])
+    if js:
+        with open(js, "w") as f:
+            json.dump(traffic_json(res), f, indent=1)
     for k, cs in res.items():
         print(f"== {k}")
         for c in sorted(cs):
