@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--chunk-blocks", type=int, default=0)
     ap.add_argument("--graph", type=int, default=1,
                     help="capture one step (3 kernel launches) in a HIP graph and replay it")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="run the step through pfb_roundtrip_execute (analysis of chunk c+1 "
+                         "on a second stream beside the synthesis of chunk c); 0 = two calls")
     ap.add_argument("--kernel-events", type=int, default=1,
                     help="record HIP events around every kernel in the timed region")
     return ap.parse_args()
@@ -125,9 +128,17 @@ def main():
     K = ana.output_length(n_dat)
     n_out = syn.output_length(K)
 
-    def step():
+    chan_buf = torch.empty((n_pol, K, N_CHAN), dtype=torch.complex64, device=dev)
+    out_buf = torch.empty((n_pol, n_out), dtype=torch.complex64, device=dev)
+
+    def step_serial():
         chan = ana.execute(x)            # (n_pol, K, N) time-major channelised data
         return syn.execute(chan, layout="ptc")
+
+    def step_pipelined():
+        return pfb.roundtrip(ana, syn, x, chan=chan_buf, out=out_buf)
+
+    step = step_pipelined if args.pipeline else step_serial
 
     lib = _lib.load()
     for _ in range(args.warmup):
@@ -169,10 +180,12 @@ def main():
     el = timed(args.steps, run)
     # profiled region: the same K steps with HIP events recorded around every kernel
     # launch on the library's launch stream (per-kernel durations for the roofline;
-    # the events add inter-kernel gaps, so this region is not used for `value`)
+    # the events add inter-kernel gaps, so this region is not used for `value`).  The
+    # kernels run one at a time here (two separate calls, one stream): a kernel's
+    # event-bracketed duration is its own, not shared with a concurrent one.
     lib.pfb_profile_reset()
     lib.pfb_profile_enable(args.kernel_events)
-    el_prof = timed(args.steps, step)
+    el_prof = timed(args.steps, step_serial)
     lib.pfb_profile_enable(0)
 
     # per-kernel-class event timings (on the library's launch stream)
@@ -222,7 +235,8 @@ def main():
                        "n_dat_per_unit": n_dat, "n_pol": n_pol, "units": world * n_pol,
                        "channelised_rows": K, "output_samples_per_unit": n_out,
                        "parallelism": f"{world} independent units, one per GPU (no collective)",
-                       "hip_graph": bool(args.graph)},
+                       "hip_graph": bool(args.graph),
+                       "pipelined": bool(args.pipeline)},
             "roofline": roof,
             "round_trip_hbm_frac": round(rt_gbs / HBM_PEAK_GBS, 4),
             "ms_per_step_with_kernel_events": round(el_prof / args.steps * 1e3, 4),

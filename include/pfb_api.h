@@ -165,6 +165,23 @@ pfb_status pfb_inverse_filterbank_reset(pfb_synthesis_plan* plan);
 /* Blocks processed per channel-IFFT/block-kernel chunk (scratch = chunk * keep rows). */
 pfb_status pfb_synthesis_set_chunk_blocks(pfb_synthesis_plan* plan, int32_t blocks);
 
+/* ---------------------------------------------------------------- round trip */
+/* Analysis followed by synthesis of its output — replaces the analysis -> synthesis
+ * sequence of test_data_pipeline.m:114,132 (and data_gen/pipeline.py:71-75).
+ * Device memory only.  in: n_pol series of n_dat samples; chan: the full channelised
+ * product (n_pol x K x n_chan, written as pfb_analysis_execute writes it); out: the
+ * synthesis of chan(:, :, sample_offset:end) as pfb_synthesis_execute computes it.
+ * Internally pipelined in chunks of synthesis blocks (pfb_synthesis_set_chunk_blocks,
+ * default 64) with the analysis on a second stream; results are bit-identical to the
+ * two separate calls.  Ordered after prior work on `stream`; later work on `stream`
+ * sees all of it (graph-capturable). */
+pfb_status pfb_roundtrip_execute(pfb_analysis_plan* analysis, pfb_synthesis_plan* synthesis,
+                                 const pfb_cf32* in, int64_t in_pol_stride, int64_t n_dat,
+                                 pfb_cf32* chan, int64_t chan_pol_stride, int64_t chan_capacity,
+                                 int64_t* n_chan_rows, int64_t sample_offset, pfb_cf32* out,
+                                 int64_t out_pol_stride, int64_t out_capacity, int64_t* n_out,
+                                 void* stream);
+
 /* ---------------------------------------------------------------- utilities */
 const char* pfb_last_error(void);
 int32_t pfb_api_version(void);

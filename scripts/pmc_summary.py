@@ -14,7 +14,7 @@ import sys
 
 
 def short(name):
-    for k in ("analysis_fused", "row_fft", "synth_block", "fir_generic"):
+    for k in ("analysis_fused", "analysis_stream", "row_fft", "synth_block", "fir_generic"):
         if k in name:
             return name.split("(")[0].replace("void pfb::", "")
     return None
@@ -32,7 +32,7 @@ def load(dirs):
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
-BENCH_NAME = {"analysis_fused": "analysis_fused", "fir_generic": "analysis_fir",
+BENCH_NAME = {"analysis_fused": "analysis_fused", "analysis_stream": "analysis_fused", "fir_generic": "analysis_fir",
               "row_fft": "synth_chan_ifft", "synth_block": "synth_block"}
 
 

@@ -1,0 +1,417 @@
+// pfb_analysis.hip — hand-written CDNA4 (gfx950) analysis kernels of the PFB round trip.
+//
+//   analysis_stream_kernel polyphase_analysis.m:83-121 for the SKA-Low shapes (N = 256):
+//                          one thread per output position c streams one column of the
+//                          input (rows of N samples) through a register window — the FIR
+//                          and the circshift need no LDS staging; T = 16 rows per step
+//                          are transformed by an N-point FFT in LDS.
+//   analysis_fused_kernel  polyphase_analysis.m:83-121 / polyphase_analysis_padded.m:106-156
+//                          for N <= 256: one workgroup = T output rows of one polarisation,
+//                          the input span staged in LDS once, the taps of the thread's
+//                          polyphase arm in registers, the circular shift applied as the
+//                          LDS write address, the N-point FFT in LDS, the last Stockham
+//                          pass writing the rows straight to HBM (coalesced).
+//   fir_generic_kernel     same maths for N > 256 (SKA-Mid 4096 channels): the FIR writes
+//                          the shifted polyphase sums, row_fft_kernel transforms them.
+#include "pfb_common.hpp"
+
+namespace pfb {
+
+// ======================================================================= analysis
+template <int N, int PMAX, int TDIV = 1>
+struct AnaShape {
+  static constexpr int T = 4096 / N / TDIV; // output rows per workgroup
+  static constexpr int RS = lds_row(N);     // padded LDS row (float2)
+  static constexpr int KSTEP = NT / N;      // rows covered by one thread sweep
+  static constexpr int KPT = T / KSTEP;     // rows per thread (= 16)
+  // input span S = M (T-1) + P N <= N (T-1) + PMAX N samples, staged as float4 pairs
+  static constexpr int SMAX = N * (T - 1) + PMAX * N;
+  static constexpr int CH = (SMAX / 2 + NT - 1) / NT;  // float4 chunks per thread
+};
+
+// Stage x[base, base + S) into LDS (zero outside [0, n_dat)).  Interior tiles issue
+// all of their 16-byte loads back to back before the first LDS write.
+template <int CH>
+__device__ __forceinline__ void stage_span(float2* smem, const float2* __restrict__ x,
+                                           int64_t base, int S, int64_t n_dat, int tid) {
+  const int S2 = (S + 1) >> 1;
+  const bool interior = base >= 0 && base + 2 * (int64_t)S2 <= n_dat &&
+                        ((reinterpret_cast<uintptr_t>(x + base) & 15) == 0);
+  if (interior) {
+    const float4* __restrict__ src = reinterpret_cast<const float4*>(x + base);
+    float4 v[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) v[i] = src[min(tid + i * NT, S2 - 1)];
+    // unconditional (clamped) stores: a guarded store lets the compiler sink each load
+    // into its branch and wait for it there, serialising the HBM latency
+#pragma unroll
+    for (int i = 0; i < CH; ++i) reinterpret_cast<float4*>(smem)[min(tid + i * NT, S2 - 1)] = v[i];
+  } else {
+    for (int s = tid; s < S; s += NT) {
+      const int64_t g = base + s;
+      smem[s] = (g >= 0 && g < n_dat) ? x[g] : make_float2(0.f, 0.f);
+    }
+  }
+}
+
+// PMAX = compile-time tap phases; EXACT means P == PMAX (no clamping needed).
+template <int N, int PMAX, int VARIANT, int TDIV, bool EXACT>
+__global__ __launch_bounds__(NT) void analysis_fused_kernel(AnalysisArgs a) {
+  static_assert(NT % N == 0, "fused analysis needs N | 256");
+  using S_ = AnaShape<N, PMAX, TDIV>;
+  constexpr int T = S_::T;
+  extern __shared__ __attribute__((aligned(16))) float2 smem[];
+  const int tid = threadIdx.x;
+  const int pol = blockIdx.y;
+  const int64_t k0 = a.row0 + (int64_t)xcd_tile(blockIdx.x, gridDim.x) * T;
+  const int M = a.M, P = a.P;
+  const int PN = P * N;
+  const int S = M * (T - 1) + PN;
+  const float2* __restrict__ x = a.in + pol * a.in_pol_stride;
+
+  // 1. this thread's polyphase arm n: taps f[m N + n] in registers (taps are padded
+  //    with zero rows to PMAX on the device, so the loads are unconditional)
+  const int n = tid % N;
+  const int kk0 = tid / N;
+  float tr[PMAX];
+#pragma unroll
+  for (int m = 0; m < PMAX; ++m) tr[m] = a.taps[m * N + n];
+  // 2. stage the input span of the T rows (Bunton: x[k0 M + s]; padded: x[k0 M - PN + s],
+  //    zero history before t = 0, polyphase_analysis_padded.m:101-102)
+  const int64_t base = (VARIANT == kBunton) ? k0 * M : k0 * M - PN;
+  stage_span<S_::CH>(smem, x, base, S, a.n_dat, tid);
+  __syncthreads();
+
+  // 3. FIR: Bunton u_k[n] = sum_m f[mN+n] x[kM + mN + n]        (polyphase_analysis.m:105-115)
+  //         padded y_q[n] = sum_p f[pN+n] x[qM - 1 - pN - n]      (polyphase_analysis_padded.m:118-126)
+  //    Branch-free: taps are zero for m >= P and the LDS read index is clamped to the
+  //    row's last phase (a sample of the row's own window, so 0 * x is exact even for
+  //    non-finite x); a guarded read would serialise every LDS access.
+  float2 u[S_::KPT];
+#pragma unroll
+  for (int e = 0; e < S_::KPT; ++e) {
+    const int k = kk0 + e * S_::KSTEP;
+    float ax = 0.f, ay = 0.f;
+    if constexpr (VARIANT == kBunton) {
+      const float2* p = smem + k * M + n;
+#pragma unroll
+      for (int m = 0; m < PMAX; ++m) {
+        const int mm = EXACT ? m : min(m, P - 1);
+        const float2 v = p[mm * N];
+        ax = fmaf(tr[m], v.x, ax);
+        ay = fmaf(tr[m], v.y, ay);
+      }
+    } else {
+      const float2* p = smem + k * M + PN - 1 - n;
+#pragma unroll
+      for (int m = 0; m < PMAX; ++m) {
+        const int mm = EXACT ? m : min(m, P - 1);
+        const float2 v = p[-mm * N];
+        ax = fmaf(tr[m], v.x, ax);
+        ay = fmaf(tr[m], v.y, ay);
+      }
+    }
+    u[e] = make_float2(ax, ay);
+  }
+  // twiddle table -> LDS, behind the FFT rows (the staged span is dead after the FIR)
+  const float2 twv = a.twN[tid & (N - 1)];
+  __syncthreads();
+  if (tid < N) smem[T * S_::RS + tid] = twv;
+
+  // 4. circular shift folded into the LDS write address
+  //    Bunton: v[(n + r) mod N] = u[n], r = (M k) mod N               (polyphase_analysis.m:102-105)
+  //    padded: z[(n - idx) mod N] = y[n], idx barrel index             (polyphase_analysis_padded.m:132-144)
+  LdsRows rows(smem, S_::RS);
+#pragma unroll
+  for (int e = 0; e < S_::KPT; ++e) {
+    const int k = kk0 + e * S_::KSTEP;
+    const int64_t kg = k0 + k;
+    int pos;
+    if constexpr (VARIANT == kBunton) {
+      const int r = (int)((kg * M) % N);
+      pos = (n + r) % N;
+    } else {
+      const int b = (int)(kg % a.nu);
+      const int idx = (b == 0) ? 0 : (int)(((int64_t)(a.nu - b) * (N - M)) % N);
+      pos = (n - idx + N) % N;
+    }
+    rows.store(k, pos, u[e]);
+  }
+  __syncthreads();
+
+  // 5. N-point DFT of every row; Bunton N*fft (forward), padded N^2*ifft (inverse dir.)
+  AnalysisStore st{a.out + pol * a.out_pol_stride, a.K, a.K_total, k0, N, a.sds, VARIANT == kPadded,
+                   (float)N};
+  block_fft<N, (VARIANT == kBunton) ? -1 : +1, T, NT>(rows, st, rows, smem + T * S_::RS, tid);
+}
+
+// ----------------------------------------------------------------------- streaming
+// Bunton analysis for N = 256 with the FIR in registers and no LDS staging of the
+// input.  View the input as rows of N samples, X[r][c] = x[r N + c].  With M = N DE/NU,
+// output row k = NU q + s (s < NU) starts at kM = DE N q + sM, and the circular shift
+// of polyphase_analysis.m:102-105 moves arm n to position (n + sM) mod N.  The thread
+// that owns position c therefore computes, for every s, arm n_s = (c - a_s) mod N with
+// a_s = sM mod N, and its samples are one COLUMN of X:
+//     v_k[c] = sum_m f[m N + n_s] X[DE q + m + b_s + e_s][c],
+//     b_s = floor(sM / N), e_s = [c < a_s].
+// Folding e_s into the taps (g_s[m'] = f[(m' - e_s) N + n_s] = F[(m' + 1) N + c - a_s]
+// with F = [N zeros, f, zeros], P + 1 taps) makes the row index DE q + m' + b_s a
+// compile-time offset into a register window that slides down the column: each input
+// sample is loaded once, coalesced (a wave reads 512 contiguous bytes of one row), and
+// the circshift costs nothing — v_k[c] is already at its shifted position.  The taps
+// are read from LDS (lane-contiguous, conflict-free; each read feeds QS rows);
+// T = 16 rows per step go to LDS for the N-point FFT.
+template <int N, int P, int NU, int DE>
+struct StreamShape {
+  static_assert(N == NT, "one thread per column");
+  static_assert(16 % NU == 0, "NU must divide 16");
+  static constexpr int M = N * DE / NU;
+  static_assert(M * NU == N * DE, "M = N de/nu must be integral");
+  static constexpr int PE = P + 1;        // taps per chain after folding e_s
+  static constexpr int QS = 16 / NU;      // commutator periods per step
+  static constexpr int T = QS * NU;       // output rows per step (16)
+  static constexpr int NEW = DE * QS;     // input rows consumed per step
+  static constexpr int WIN = NEW + PE - 1;  // register window (rows)
+  static constexpr int RS = lds_row(N);
+  static constexpr int TW_OFF = T * RS;               // float2 offset of the twiddles
+  static constexpr int F_OFF = 2 * (TW_OFF + N);      // float offset of the taps F
+  static constexpr int F_LEN = (P + 2) * N;
+  static constexpr size_t lds_bytes = (size_t)F_OFF * sizeof(float) + F_LEN * sizeof(float);
+};
+
+template <int N, int P, int NU, int DE>
+__global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
+  using SH = StreamShape<N, P, NU, DE>;
+  constexpr int M = SH::M, PE = SH::PE, QS = SH::QS, T = SH::T, NEW = SH::NEW, WIN = SH::WIN;
+  extern __shared__ __attribute__((aligned(16))) float2 smem[];
+  const int c = threadIdx.x;
+  const int pol = blockIdx.y;
+  // this workgroup's steps (XCD-aware order: neighbouring ranges share halo rows in L2)
+  const int64_t q_lo = a.row0 / NU;
+  const int64_t n_steps = ((a.K + NU - 1) / NU - q_lo + QS - 1) / QS;
+  const int w = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t st0 = n_steps * w / gridDim.x, st1 = n_steps * (w + 1) / gridDim.x;
+  if (st0 >= st1) return;
+
+  // input column c from row DE q_first on; range-checked buffer loads return 0 past n_dat
+  const int64_t row_first = (int64_t)DE * (q_lo + st0 * QS);
+  const float2* xpol = a.in + pol * a.in_pol_stride;
+  const int64_t avail = a.n_dat - row_first * N;
+  uint32_t nbytes = (uint32_t)min(max(avail, (int64_t)0) * 8, (int64_t)0x7ffffff0);
+  if (a.timing_mask & 1) nbytes = 0;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(xpol + row_first * N, nbytes);
+  auto ld = [&](int r) {  // window row r (relative to row_first)
+    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (r * N + c) * 8, 0, 0);
+    return __builtin_bit_cast(float2, v);
+  };
+  float2 win[WIN];
+#pragma unroll
+  for (int i = 0; i < WIN; ++i) win[i] = ld(i);
+
+  // LDS: twiddles behind the FFT rows, then F = [N zeros, taps, zeros]
+  float* F = reinterpret_cast<float*>(smem) + SH::F_OFF;
+  smem[SH::TW_OFF + c] = a.twN[c];
+#pragma unroll
+  for (int m = 0; m < P + 2; ++m) F[m * N + c] = (m >= 1 && m <= P) ? a.taps[(m - 1) * N + c] : 0.f;
+
+  AnalysisStore st{a.out + pol * a.out_pol_stride, a.K, a.K_total, 0, N, a.sds, 0, (float)N, a.row0};
+  LdsRows rows(smem, SH::RS);
+  const float2* tw = smem + SH::TW_OFF;
+#pragma unroll 1
+  for (int64_t stp = st0; stp < st1; ++stp) {
+    const int rel = (int)(stp - st0) * NEW;  // window row 0 of this step
+    // prefetch the next step's new rows (consumed when the window slides)
+    float2 pf[NEW];
+    if (stp + 1 < st1) {
+#pragma unroll
+      for (int i = 0; i < NEW; ++i) pf[i] = ld(rel + WIN + i);
+    }
+    __syncthreads();  // previous step's FFT has read its rows (first step: F staged)
+    // all NU x QS rows accumulate together (tap-outer order): consecutive FMAs are
+    // independent, so the 4-cycle FMA latency never stalls issue
+    float2 acc[NU][QS];
+    static_for<0, NU>([&](auto sv) {
+#pragma unroll
+      for (int qq = 0; qq < QS; ++qq) acc[decltype(sv)::value][qq] = make_float2(0.f, 0.f);
+    });
+    static_for<0, PE>([&](auto mv) {
+      constexpr int m = decltype(mv)::value;
+      float gm[NU];
+      static_for<0, NU>([&](auto sv) {
+        constexpr int s = decltype(sv)::value;
+        gm[s] = F[(m + 1) * N + c - (s * M) % N];
+      });
+      if ((a.timing_mask & 2) && m > 0) return;
+      static_for<0, NU>([&](auto sv) {
+        constexpr int s = decltype(sv)::value;
+        constexpr int bs = (s * M) / N;
+        static_for<0, QS>([&](auto qv) {
+          constexpr int qq = decltype(qv)::value;
+          const float2 v = win[DE * qq + m + bs];
+          acc[s][qq].x = fmaf(gm[s], v.x, acc[s][qq].x);
+          acc[s][qq].y = fmaf(gm[s], v.y, acc[s][qq].y);
+        });
+      });
+    });
+    static_for<0, NU>([&](auto sv) {
+      constexpr int s = decltype(sv)::value;
+      static_for<0, QS>([&](auto qv) {
+        constexpr int qq = decltype(qv)::value;
+        rows.store(qq * NU + s, c, acc[s][qq]);
+      });
+    });
+    __syncthreads();
+    st.k0 = (q_lo + stp * QS) * NU;
+    if (a.timing_mask & 8) st.K = 0;
+    if (a.timing_mask & 4) {
+#pragma unroll
+      for (int r = 0; r < T; ++r) st.store(r, c, rows.load(r, c));
+    } else {
+      block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
+    }
+#pragma unroll
+    for (int i = 0; i < PE - 1; ++i) win[i] = win[i + NEW];
+#pragma unroll
+    for (int i = 0; i < NEW; ++i) win[PE - 1 + i] = pf[i];
+  }
+}
+
+template <int VARIANT>
+__global__ __launch_bounds__(NT) void fir_generic_kernel(AnalysisArgs a) {
+  const int pol = blockIdx.y;
+  const int N = a.N, M = a.M, P = a.P;
+  const int64_t idx = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (idx >= (a.K - a.row0) * N) return;
+  const int64_t kl = idx / N;  // row within the launch
+  const int64_t k = a.row0 + kl;
+  const int n = (int)(idx - kl * N);
+  const float2* __restrict__ x = a.in + pol * a.in_pol_stride;
+  float ax = 0.f, ay = 0.f;
+  for (int m = 0; m < P; ++m) {
+    const float f = a.taps[m * N + n];
+    int64_t g;
+    if constexpr (VARIANT == kBunton) g = k * M + (int64_t)m * N + n;
+    else g = k * M - 1 - (int64_t)m * N - n;
+    if (g >= 0 && g < a.n_dat) {
+      const float2 v = x[g];
+      ax = fmaf(f, v.x, ax);
+      ay = fmaf(f, v.y, ay);
+    }
+  }
+  int pos;
+  if constexpr (VARIANT == kBunton) {
+    pos = (int)((n + (k * M) % N) % N);
+  } else {
+    const int b = (int)(k % a.nu);
+    const int ix = (b == 0) ? 0 : (int)(((int64_t)(a.nu - b) * (N - M)) % N);
+    pos = (n - ix + N) % N;
+  }
+  a.scratch[(int64_t)pol * (a.K - a.row0) * N + kl * N + pos] = make_float2(ax, ay);
+}
+
+template <int N, int PMAX, int VARIANT, int TDIV, bool EXACT = false>
+static hipError_t launch_fused(const AnalysisArgs& a, hipStream_t s) {
+  using S_ = AnaShape<N, PMAX, TDIV>;
+  const size_t span = (size_t)a.M * (S_::T - 1) + (size_t)a.P * N;
+  const size_t rows = (size_t)S_::T * S_::RS + N;  // FFT rows + twiddle table
+  const size_t bytes = ((span + 1 > rows) ? span + 1 : rows) * sizeof(float2);
+  auto kern = analysis_fused_kernel<N, PMAX, VARIANT, TDIV, EXACT>;
+  hipError_t e = set_lds(kern, bytes);
+  if (e != hipSuccess) return e;
+  dim3 grid((unsigned)((a.K - a.row0 + S_::T - 1) / S_::T), (unsigned)a.n_pol);
+  hipLaunchKernelGGL(kern, grid, dim3(NT), bytes, s, a);
+  return hipGetLastError();
+}
+
+template <int N, int P, int NU, int DE>
+static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
+  using SH = StreamShape<N, P, NU, DE>;
+  auto kern = analysis_stream_kernel<N, P, NU, DE>;
+  hipError_t e = set_lds(kern, SH::lds_bytes);
+  if (e != hipSuccess) return e;
+  const int64_t q_lo = a.row0 / NU;
+  const int64_t n_steps = ((a.K + NU - 1) / NU - q_lo + SH::QS - 1) / SH::QS;
+  // LDS-limited resident workgroups per CU, each a contiguous range of steps
+  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / SH::lds_bytes));
+  const int64_t per_pol = std::max<int64_t>(1, (per_cu * cu_count()) / a.n_pol);
+  const int64_t wgs = std::min<int64_t>(n_steps, per_pol);
+  dim3 grid((unsigned)wgs, (unsigned)a.n_pol);
+  hipLaunchKernelGGL(kern, grid, dim3(NT), SH::lds_bytes, s, a);
+  return hipGetLastError();
+}
+
+// streaming kernel for the SKA-Low shapes (N = 256, Bunton); 0 = not compiled
+static bool stream_shape(const AnalysisArgs& a) {
+  if (a.variant != kBunton || a.N != 256) return false;
+  if (a.nu == 8 && a.M == 224) return a.P == 13 || a.P == 12;
+  if (a.nu == 4 && a.M == 192) return a.P == 13 || a.P == 12;
+  return false;
+}
+
+static hipError_t launch_stream_any(const AnalysisArgs& a, hipStream_t s) {
+  if (a.nu == 8) return a.P == 13 ? launch_stream<256, 13, 8, 7>(a, s) : launch_stream<256, 12, 8, 7>(a, s);
+  return a.P == 13 ? launch_stream<256, 13, 4, 3>(a, s) : launch_stream<256, 12, 4, 3>(a, s);
+}
+
+template <int N, int VARIANT>
+static hipError_t launch_fused_p(const AnalysisArgs& a, hipStream_t s) {
+  // exact instantiations for the configured tap counts (SKA-Low 13 and 12 phases,
+  // the 'test' config 11); other P use the clamped PMAX 16/32 kernels
+  if (a.P == 13) return launch_fused<N, 13, VARIANT, 1, true>(a, s);
+  if (a.P == 12) return launch_fused<N, 12, VARIANT, 1, true>(a, s);
+  if (a.P == 11) return launch_fused<N, 11, VARIANT, 1, true>(a, s);
+  if (a.P <= 16) return launch_fused<N, 16, VARIANT, 1>(a, s);
+  return launch_fused<N, 32, VARIANT, 1>(a, s);
+}
+
+template <int N>
+static hipError_t launch_fused_v(const AnalysisArgs& a, hipStream_t s) {
+  if (a.variant == kBunton) return launch_fused_p<N, kBunton>(a, s);
+  return launch_fused_p<N, kPadded>(a, s);
+}
+
+bool analysis_supported(int N, int P, int variant, bool* fused) {
+  (void)variant;
+  const bool f = (N >= 8 && N <= 256 && pow2_supported(N) && P <= 32);
+  if (fused) *fused = f;
+  return pow2_supported(N);
+}
+
+hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
+  if (a.K <= a.row0) return hipSuccess;
+  bool fused = false;
+  if (!analysis_supported(a.N, a.P, a.variant, &fused)) return hipErrorInvalidValue;
+  static const bool no_stream = std::getenv("PFB_ANALYSIS_NO_STREAM") != nullptr;
+  if (fused && stream_shape(a) && !no_stream) {
+    static const int mask = std::getenv("PFB_ANA_MASK") ? std::atoi(std::getenv("PFB_ANA_MASK")) : 0;
+    AnalysisArgs b = a;
+    b.timing_mask = mask;
+    return launch_stream_any(b, s);
+  }
+  if (fused) {
+    switch (a.N) {
+      case 8: return launch_fused_v<8>(a, s);
+      case 16: return launch_fused_v<16>(a, s);
+      case 32: return launch_fused_v<32>(a, s);
+      case 64: return launch_fused_v<64>(a, s);
+      case 128: return launch_fused_v<128>(a, s);
+      case 256: return launch_fused_v<256>(a, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if (!a.scratch) return hipErrorInvalidValue;
+  // generic: FIR into scratch, then row FFT (with the padded circular time shift)
+  const int64_t rows = a.K - a.row0;
+  const int64_t total = rows * a.N;
+  dim3 grid((unsigned)((total + NT - 1) / NT), (unsigned)a.n_pol);
+  if (a.variant == kBunton) hipLaunchKernelGGL(fir_generic_kernel<kBunton>, grid, dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(fir_generic_kernel<kPadded>, grid, dim3(NT), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  RowFftArgs r{a.scratch, rows * a.N, a.out, a.out_pol_stride, rows, nullptr, nullptr, a.twN,
+               (float)a.N, a.sds, a.variant == kPadded, a.row0, a.K_total};
+  if (a.variant == kBunton) return dispatch_row_fft<-1>(a.N, r, a.n_pol, s);
+  return dispatch_row_fft<+1>(a.N, r, a.n_pol, s);
+}
+
+}  // namespace pfb

@@ -149,22 +149,31 @@ struct pfb_analysis_plan {
   int variant = 0, N = 0, nu = 1, de = 1, M = 0, P = 0, n_pol = 1, sds = 0;
   int64_t n_taps = 0;
   bool fused = false;
-  int strips = 0;  // PFB_ANALYSIS_STRIPS (experiment knob): persistent workgroups per pol
   DevBuf taps, twN, scratch;
   // streaming (FilterBank.m:13-14 input_buffer / buffered_samples)
   DevBuf carry, work, stage_in, stage_out;
   int64_t buffered = 0;
+  // round trip (pfb_roundtrip_execute): the analysis runs on this stream, ahead of the
+  // synthesis on the caller's stream; one event per chunk orders them
+  hipStream_t aux = nullptr;
+  std::vector<hipEvent_t> events;
 };
 
+// Rows [row0, K_end) of a call whose output has K_total rows per pol (the padded
+// variant's circular shift is modulo K_total).  `in`/`out` are the call's bases.
 static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
-                               float2* out, int64_t out_ps, int64_t K, hipStream_t s) {
+                               float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
+                               int64_t K_total, hipStream_t s) {
+  if (K_end <= row0) return PFB_OK;
   pfb::AnalysisArgs a{};
   a.in = in;
   a.in_pol_stride = in_ps;
   a.n_dat = n_dat;
   a.out = out;
   a.out_pol_stride = out_ps;
-  a.K = K;
+  a.row0 = row0;
+  a.K = K_end;
+  a.K_total = K_total;
   a.n_pol = p->n_pol;
   a.N = p->N;
   a.M = p->M;
@@ -175,12 +184,16 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   a.taps = p->taps.as<float>();
   a.twN = p->twN.as<float2>();
   a.scratch = nullptr;
-  a.strips = p->strips;
   if (!p->fused) {
-    HIPCHK(p->scratch.ensure((size_t)p->n_pol * K * p->N * sizeof(float2)));
+    HIPCHK(p->scratch.ensure((size_t)p->n_pol * (K_end - row0) * p->N * sizeof(float2)));
     a.scratch = p->scratch.as<float2>();
   }
-  const double bytes = (double)p->n_pol * (8.0 * n_dat + 8.0 * K * p->N);
+  // algorithmic bytes: each input sample read once (the rows' new samples, the tail of
+  // the series with the last rows), each output sample written once
+  const int64_t in_samples = (K_end == K_total && row0 == 0)
+                                 ? n_dat
+                                 : (K_end - row0) * p->M + (K_end == K_total ? n_dat - K_total * p->M : 0);
+  const double bytes = (double)p->n_pol * (8.0 * in_samples + 8.0 * (K_end - row0) * p->N);
   ProfScope ps(0, bytes, s);
   HIPCHK(pfb::launch_analysis(a, s));
   return PFB_OK;
@@ -243,7 +256,6 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
     delete p;
     return fail(PFB_ERR_HIP, "hipSetDevice(%d) failed", d->device);
   }
-  if (const char* v = std::getenv("PFB_ANALYSIS_STRIPS")) p->strips = std::max(0, std::atoi(v));
   // zero rows up to the fused kernel's PMAX (32) so its tap loads are unconditional
   std::vector<float> taps((size_t)std::max(p->P, 32) * p->N, 0.f);
   for (int64_t i = 0; i < d->n_taps; ++i) taps[(size_t)i] = (float)d->taps[i];  // cast(filt, 'single')
@@ -267,6 +279,8 @@ pfb_status pfb_analysis_plan_destroy(pfb_analysis_plan* p) {
   p->work.release();
   p->stage_in.release();
   p->stage_out.release();
+  for (hipEvent_t e : p->events) (void)hipEventDestroy(e);
+  if (p->aux) (void)hipStreamDestroy(p->aux);
   delete p;
   return PFB_OK;
 }
@@ -292,7 +306,7 @@ pfb_status pfb_analysis_execute(pfb_analysis_plan* p, const pfb_cf32* in, int64_
   if (mem == PFB_MEM_DEVICE) {
     if (in_ps < n_dat || out_ps < K * p->N)
       return fail(PFB_ERR_INVALID_ARG, "polarisation stride smaller than the data");
-    return analysis_run(p, (const float2*)in, in_ps, n_dat, (float2*)out, out_ps, K, s);
+    return analysis_run(p, (const float2*)in, in_ps, n_dat, (float2*)out, out_ps, 0, K, K, s);
   }
   // host staging (synchronous)
   HIPCHK(p->stage_in.ensure((size_t)p->n_pol * n_dat * sizeof(float2)));
@@ -301,7 +315,7 @@ pfb_status pfb_analysis_execute(pfb_analysis_plan* p, const pfb_cf32* in, int64_
     HIPCHK(hipMemcpyAsync(p->stage_in.as<float2>() + (size_t)q * n_dat, in + q * in_ps,
                           n_dat * sizeof(float2), hipMemcpyHostToDevice, s));
   pfb_status st = analysis_run(p, p->stage_in.as<float2>(), n_dat, n_dat,
-                               p->stage_out.as<float2>(), K * p->N, K, s);
+                               p->stage_out.as<float2>(), K * p->N, 0, K, K, s);
   if (st != PFB_OK) return st;
   for (int q = 0; q < p->n_pol; ++q)
     HIPCHK(hipMemcpyAsync(out + q * out_ps, p->stage_out.as<float2>() + (size_t)q * K * p->N,
@@ -350,7 +364,7 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
         dps = K * p->N;
       }
     }
-    pfb_status st = analysis_run(p, w, total, total, dst, dps, K, s);
+    pfb_status st = analysis_run(p, w, total, total, dst, dps, 0, K, K, s);
     if (st != PFB_OK) return st;
     if (dst != (float2*)out) {
       const hipMemcpyKind ko = mem == PFB_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
@@ -391,6 +405,7 @@ struct pfb_synthesis_plan {
   int W = 0, keep = 0, L = 0, Lov = 0, Lkeep = 0, t1_lo = 0, t1_hi = 0;
   bool deripple = false;
   int chunk_blocks = 0;
+  int rt_chunk_blocks = 64;  // round-trip pipeline chunk (PFB_RT_CHUNK_BLOCKS)
   int timing_mask = 0;  // PFB_TIMING_MASK (timing experiments; results invalid when set)
   int ranges = -1;  // PFB_SYNTH_RANGES: 0 one workgroup per block, -1 persistent auto, >0 persistent
   bool identity_perm = true;
@@ -414,10 +429,63 @@ static int64_t synth_blocks(const pfb_synthesis_plan* p, int64_t n_dat) {
   return std::max<int64_t>(b, 0);
 }
 
-static pfb_status synthesis_run(pfb_synthesis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
-                                float2* out, int64_t out_ps, int64_t out_limit, hipStream_t s) {
-  const int64_t B = synth_blocks(p, n_dat);
-  if (B == 0) return PFB_OK;
+// Blocks [b0, b0 + nb) of a call: channel IFFT of their rows into Z, then the block
+// kernel.  `in` is the call's first channelised row (sample_offset applied).
+static pfb_status synthesis_chunk(pfb_synthesis_plan* p, const float2* in, int64_t in_ps, int64_t b0,
+                                  int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
+                                  hipStream_t s) {
+  const int64_t rows = nb * p->keep + 2 * (int64_t)p->Ov;
+  HIPCHK(p->Z.ensure((size_t)p->n_pol * rows * p->N * sizeof(float2)));
+  float2* Z = p->Z.as<float2>();
+  pfb::ChanIfftArgs c{};
+  c.in = in + b0 * p->keep * p->N;
+  c.in_pol_stride = in_ps;
+  c.out = Z;
+  c.out_pol_stride = rows * p->N;
+  c.n_rows = rows;
+  c.n_pol = p->n_pol;
+  c.N = p->N;
+  c.perm = p->identity_perm ? nullptr : p->perm.as<int>();
+  c.cgain = p->has_cgain ? p->cgain.as<float>() : nullptr;
+  c.twN = p->twN.as<float2>();
+  {
+    ProfScope ps(1, (double)p->n_pol * rows * p->N * 16.0, s);
+    HIPCHK(pfb::launch_chan_ifft(c, s));
+  }
+  pfb::SynthBlockArgs a{};
+  a.Z = Z;
+  a.z_pol_stride = rows * p->N;
+  a.out = out;
+  a.out_pol_stride = out_ps;
+  a.block0 = b0;
+  a.n_blocks = (int)nb;
+  a.n_pol = p->n_pol;
+  a.N = p->N;
+  a.Nf = p->Nf;
+  a.W = p->W;
+  a.keep = p->keep;
+  a.L = p->L;
+  a.Lov = p->Lov;
+  a.Lkeep = p->Lkeep;
+  a.t1_lo = p->t1_lo;
+  a.t1_hi = p->t1_hi;
+  a.scale = (float)((double)p->de / (double)p->nu / (double)p->L);
+  a.window = p->window.as<float>();
+  a.spans = p->spans;
+  a.tw4 = p->tw4.as<float2>();
+  a.twNf = p->twNf.as<float2>();
+  a.twW = p->twW.as<float2>();
+  a.out_limit = out_limit;
+  a.ranges = p->ranges;
+  a.timing_mask = p->timing_mask;
+  {
+    ProfScope ps(2, (double)p->n_pol * (nb * p->keep * p->N * 8.0 + nb * p->Lkeep * 8.0), s);
+    HIPCHK(pfb::launch_synth_block(a, s));
+  }
+  return PFB_OK;
+}
+
+static int64_t synthesis_chunk_blocks(const pfb_synthesis_plan* p, int64_t B) {
   int64_t CB = p->chunk_blocks;
   if (CB <= 0) {
     // one chunk up to 2^26 channel-rows x channels (512 MB of Z); fewer, larger
@@ -425,58 +493,18 @@ static pfb_status synthesis_run(pfb_synthesis_plan* p, const float2* in, int64_t
     const int64_t target = (int64_t)1 << 26;
     CB = std::max<int64_t>(1, target / ((int64_t)p->keep * p->N * p->n_pol));
   }
-  CB = std::min<int64_t>(CB, B);
-  const int64_t zrows = CB * p->keep + 2 * (int64_t)p->Ov;
-  HIPCHK(p->Z.ensure((size_t)p->n_pol * zrows * p->N * sizeof(float2)));
-  float2* Z = p->Z.as<float2>();
+  return std::min<int64_t>(CB, B);
+}
+
+static pfb_status synthesis_run(pfb_synthesis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
+                                float2* out, int64_t out_ps, int64_t out_limit, hipStream_t s) {
+  const int64_t B = synth_blocks(p, n_dat);
+  if (B == 0) return PFB_OK;
+  const int64_t CB = synthesis_chunk_blocks(p, B);
   for (int64_t b0 = 0; b0 < B; b0 += CB) {
-    const int64_t nb = std::min<int64_t>(CB, B - b0);
-    const int64_t rows = nb * p->keep + 2 * (int64_t)p->Ov;
-    pfb::ChanIfftArgs c{};
-    c.in = in + b0 * p->keep * p->N;
-    c.in_pol_stride = in_ps;
-    c.out = Z;
-    c.out_pol_stride = zrows * p->N;
-    c.n_rows = rows;
-    c.n_pol = p->n_pol;
-    c.N = p->N;
-    c.perm = p->identity_perm ? nullptr : p->perm.as<int>();
-    c.cgain = p->has_cgain ? p->cgain.as<float>() : nullptr;
-    c.twN = p->twN.as<float2>();
-    {
-      ProfScope ps(1, (double)p->n_pol * rows * p->N * 16.0, s);
-      HIPCHK(pfb::launch_chan_ifft(c, s));
-    }
-    pfb::SynthBlockArgs a{};
-    a.Z = Z;
-    a.z_pol_stride = zrows * p->N;
-    a.out = out;
-    a.out_pol_stride = out_ps;
-    a.block0 = b0;
-    a.n_blocks = (int)nb;
-    a.n_pol = p->n_pol;
-    a.N = p->N;
-    a.Nf = p->Nf;
-    a.W = p->W;
-    a.keep = p->keep;
-    a.L = p->L;
-    a.Lov = p->Lov;
-    a.Lkeep = p->Lkeep;
-    a.t1_lo = p->t1_lo;
-    a.t1_hi = p->t1_hi;
-    a.scale = (float)((double)p->de / (double)p->nu / (double)p->L);
-    a.window = p->window.as<float>();
-    a.spans = p->spans;
-    a.tw4 = p->tw4.as<float2>();
-    a.twNf = p->twNf.as<float2>();
-    a.twW = p->twW.as<float2>();
-    a.out_limit = out_limit;
-    a.ranges = p->ranges;
-    a.timing_mask = p->timing_mask;
-    {
-      ProfScope ps(2, (double)p->n_pol * (nb * p->keep * p->N * 8.0 + nb * p->Lkeep * 8.0), s);
-      HIPCHK(pfb::launch_synth_block(a, s));
-    }
+    pfb_status st = synthesis_chunk(p, in, in_ps, b0, std::min<int64_t>(CB, B - b0), out, out_ps,
+                                    out_limit, s);
+    if (st != PFB_OK) return st;
   }
   return PFB_OK;
 }
@@ -518,6 +546,7 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
   p->device = d->device;
   if (const char* v = std::getenv("PFB_SYNTH_RANGES")) p->ranges = std::max(-1, std::atoi(v));
   if (const char* v = std::getenv("PFB_TIMING_MASK")) p->timing_mask = std::atoi(v);
+  if (const char* v = std::getenv("PFB_RT_CHUNK_BLOCKS")) p->rt_chunk_blocks = std::max(1, std::atoi(v));
   p->N = N;
   p->nu = nu;
   p->de = de;
@@ -789,6 +818,83 @@ int64_t pfb_inverse_filterbank_buffered(const pfb_synthesis_plan* p) { return p 
 pfb_status pfb_inverse_filterbank_reset(pfb_synthesis_plan* p) {
   if (!p) return fail(PFB_ERR_INVALID_ARG, "null plan");
   p->buffered = 0;
+  return PFB_OK;
+}
+
+// ------------------------------------------------------------------ round trip
+// Analysis -> synthesis of one call, pipelined in chunks of synthesis blocks (the
+// reference's test_data_pipeline.m:114,132 runs the two back to back).  Chunk c's
+// analysis rows run on the analysis plan's own stream while chunk c-1 is synthesised
+// on the caller's stream, so the two kernels share the chip (each alone leaves HBM and
+// VALU partly idle), and the synthesis reads each channelised row shortly after it was
+// written (Infinity-Cache resident).  The full channelised product is still written to
+// `chan`.  Every row and block is computed by the same kernels with the same inputs as
+// pfb_analysis_execute + pfb_synthesis_execute, so the results are bit-identical.
+pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, const pfb_cf32* in,
+                                 int64_t in_ps, int64_t n_dat, pfb_cf32* chan, int64_t chan_ps,
+                                 int64_t chan_cap, int64_t* n_chan_rows, int64_t sample_offset,
+                                 pfb_cf32* out, int64_t out_ps, int64_t out_cap, int64_t* n_out,
+                                 void* stream) {
+  if (!pa || !ps || (!in && n_dat > 0)) return fail(PFB_ERR_INVALID_ARG, "null argument");
+  if (pa->device != ps->device) return fail(PFB_ERR_INVALID_ARG, "plans on different devices");
+  if (pa->N != ps->N || pa->n_pol != ps->n_pol)
+    return fail(PFB_ERR_INVALID_ARG, "analysis (%d ch, %d pol) and synthesis (%d ch, %d pol) differ",
+                pa->N, pa->n_pol, ps->N, ps->n_pol);
+  if (sample_offset < 1) return fail(PFB_ERR_INVALID_ARG, "sample_offset is 1-based (>= 1)");
+  if (n_dat < 0) return fail(PFB_ERR_INVALID_ARG, "negative n_dat");
+  HIPCHK(hipSetDevice(pa->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t K = analysis_K(pa, n_dat);
+  const int64_t off = std::min<int64_t>(sample_offset - 1, K);
+  const int64_t B = synth_blocks(ps, K - off);
+  const int64_t olen = B * ps->Lkeep;
+  if (n_chan_rows) *n_chan_rows = K;
+  if (n_out) *n_out = olen;
+  if (K == 0) return PFB_OK;
+  if (!chan || (olen > 0 && !out)) return fail(PFB_ERR_INVALID_ARG, "null output");
+  if (chan_cap < K) return fail(PFB_ERR_BUFFER_TOO_SMALL, "channelised capacity %lld < %lld rows",
+                                (long long)chan_cap, (long long)K);
+  if (out_cap < olen) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld",
+                                  (long long)out_cap, (long long)olen);
+  if (in_ps < n_dat || chan_ps < K * pa->N || (olen > 0 && out_ps < olen))
+    return fail(PFB_ERR_INVALID_ARG, "polarisation stride smaller than the data");
+  const float2* x = (const float2*)in;
+  float2* y = (float2*)chan;
+  if (B == 0) return analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s);
+
+  if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));
+  int64_t CB = ps->chunk_blocks > 0 ? ps->chunk_blocks : ps->rt_chunk_blocks;
+  CB = std::max<int64_t>(1, std::min<int64_t>(CB, B));
+  const int64_t n_chunks = (B + CB - 1) / CB;
+  while ((int64_t)pa->events.size() < n_chunks + 2) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    pa->events.push_back(e);
+  }
+  // fork: the analysis stream starts after everything already queued on the caller's
+  HIPCHK(hipEventRecord(pa->events[0], s));
+  HIPCHK(hipStreamWaitEvent(pa->aux, pa->events[0], 0));
+  const float2* sin_ = y + off * pa->N;  // synthesis input = chan(:, :, sample_offset:end)
+  int64_t ra = 0;                        // analysis rows done
+  for (int64_t c = 0; c < n_chunks; ++c) {
+    const int64_t b0 = c * CB, nb = std::min<int64_t>(CB, B - b0);
+    // channelised rows the chunk reads: [off + b0 keep, off + (b0+nb) keep + 2 Ov); the
+    // padded variant's output row t comes from analysis row (t + sds) mod K (rows that
+    // wrap come from the first rows, produced by chunk 0)
+    int64_t need = (c == n_chunks - 1) ? K : off + (b0 + nb) * ps->keep + 2 * (int64_t)ps->Ov;
+    if (pa->variant == pfb::kPadded) need += pa->sds;
+    const int64_t rb = std::max(ra, std::min(K, need));
+    pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, ra, rb, K, pa->aux);
+    if (st != PFB_OK) return st;
+    ra = rb;
+    HIPCHK(hipEventRecord(pa->events[1 + c], pa->aux));
+    HIPCHK(hipStreamWaitEvent(s, pa->events[1 + c], 0));
+    st = synthesis_chunk(ps, sin_, chan_ps, b0, nb, (float2*)out, out_ps, olen, s);
+    if (st != PFB_OK) return st;
+  }
+  // join (the last chunk already ran the analysis to K)
+  HIPCHK(hipEventRecord(pa->events[1 + n_chunks], pa->aux));
+  HIPCHK(hipStreamWaitEvent(s, pa->events[1 + n_chunks], 0));
   return PFB_OK;
 }
 

@@ -1,0 +1,166 @@
+// pfb_common.hpp — pieces shared by the kernel translation units (pfb_analysis.hip,
+// pfb_rowfft.hip, pfb_synth.hip): workgroup size, store/load functors, the XCD-aware
+// tile order, the row-FFT kernel template and launch helpers.
+#pragma once
+
+#include "pfb_device.hpp"
+#include "pfb_kernels.hpp"
+#include "pfb_pair.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace pfb {
+
+constexpr int NT = 256;  // threads per workgroup (4 wave64)
+
+// ======================================================================= functors
+struct AnalysisStore {
+  static constexpr bool kIsLds = false;
+  float2* out;
+  int64_t K, Ktot, k0;  // K: end of the launch's rows; Ktot: rows of the whole call
+  int N, sds, padded;
+  float scale;
+  int64_t k_lo = 0;     // first row of the launch (rows below it belong to another launch)
+  __device__ __forceinline__ void store(int row, int c, float2 v) const {
+    const int64_t kg = k0 + row;
+    if (kg < K && kg >= k_lo) {
+      int64_t t = kg;
+      if (padded) {
+        t = (kg - sds) % Ktot;
+        if (t < 0) t += Ktot;
+      }
+      out[t * N + c] = cscale(v, scale);
+    }
+  }
+};
+
+// Row loader of the first FFT pass.  Rows past the end are clamped to the last valid
+// row (their results are never stored), so every load is unconditional and the
+// compiler can issue them back to back.
+template <bool PERM, bool GAIN>
+struct RowLoad {
+  static constexpr bool kIsLds = false;
+  const float2* in;
+  int64_t r0, last;
+  int N;
+  const int* perm;
+  const float* cgain;
+  __device__ __forceinline__ float2 load(int row, int i) const {
+    const int64_t r = min(r0 + row, last);
+    const int c = PERM ? perm[i] : i;
+    float2 v = in[r * N + c];
+    if constexpr (GAIN) v = cscale(v, cgain[c]);  // taper acts on input rows (before re-ordering)
+    return v;
+  }
+};
+
+struct RowStore {
+  static constexpr bool kIsLds = false;
+  float2* out;
+  int64_t r0, n_rows;
+  int N;
+  int64_t sds;
+  int remap;
+  float scale;
+  int64_t row_base, n_total;  // output row = row_base + r (circularly shifted by -sds mod n_total)
+  __device__ __forceinline__ void store(int row, int c, float2 v) const {
+    const int64_t r = r0 + row;
+    if (r < n_rows) {
+      int64_t t = row_base + r;
+      if (remap) {
+        t = (t - sds) % n_total;
+        if (t < 0) t += n_total;
+      }
+      out[t * N + c] = cscale(v, scale);
+    }
+  }
+};
+
+// XCD-aware tile order: workgroups b and b+8 share an XCD (and its L2); give them
+// consecutive tiles so the halo of one tile is an L2 hit for its neighbour.
+// Bijective for any grid size (cdna_hip_programming.md, "XCD swizzle must be bijective").
+__device__ __forceinline__ int xcd_tile(int b, int nwg) {
+  const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+// ======================================================================= row FFT
+struct RowFftArgs {
+  const float2* in;
+  int64_t in_pol_stride;
+  float2* out;
+  int64_t out_pol_stride;
+  int64_t n_rows;
+  const int* perm;
+  const float* cgain;
+  const float2* tw;
+  float scale;
+  int64_t sds;
+  int remap;
+  int64_t row_base;  // global index of row 0 (output row = row_base + r, then the remap)
+  int64_t n_total;   // rows of the whole call (remap modulus)
+};
+
+template <int N>
+struct RowShape {
+  static constexpr int ROWS = (N >= 4096) ? 1 : 4096 / N;
+  static constexpr int RS = lds_row(N);
+};
+
+template <int N, int DIR, bool PERM, bool GAIN>
+__global__ __launch_bounds__(NT) void row_fft_kernel(RowFftArgs a) {
+  constexpr int ROWS = RowShape<N>::ROWS;
+  extern __shared__ __attribute__((aligned(16))) float2 smem[];
+  const int pol = blockIdx.y;
+  const int64_t r0 = (int64_t)blockIdx.x * ROWS;
+  RowLoad<PERM, GAIN> ld{a.in + pol * a.in_pol_stride, r0, a.n_rows - 1, N, a.perm, a.cgain};
+  RowStore st{a.out + pol * a.out_pol_stride, r0, a.n_rows, N, a.sds, a.remap, a.scale,
+              a.row_base, a.n_total};
+  LdsRows rows(smem, RowShape<N>::RS);
+  // twiddle table -> LDS behind the rows (ordered before pass 2 by its barrier)
+  float2* tw = smem + ROWS * RowShape<N>::RS;
+  constexpr int TPT = (N + NT - 1) / NT;
+  float2 twv[TPT];
+#pragma unroll
+  for (int i = 0; i < TPT; ++i) twv[i] = a.tw[(threadIdx.x + i * NT) & (N - 1)];
+#pragma unroll
+  for (int i = 0; i < TPT; ++i)
+    if (threadIdx.x + i * NT < N) tw[threadIdx.x + i * NT] = twv[i];
+  block_fft<N, DIR, ROWS, NT>(ld, st, rows, tw, threadIdx.x);
+}
+
+
+// ======================================================================= launchers
+template <class K>
+inline hipError_t set_lds(K kernel, size_t bytes) {
+  if (bytes > 65536) {
+    return hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bytes);
+  }
+  return hipSuccess;
+}
+
+inline int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+
+inline bool pow2_supported(int N) {
+  return N == 8 || N == 16 || N == 32 || N == 64 || N == 128 || N == 256 || N == 512 ||
+         N == 1024 || N == 2048 || N == 4096;
+}
+
+
+// N-point row FFT over n_rows rows (pfb_rowfft.hip); DIR -1 forward, +1 inverse.
+template <int DIR>
+hipError_t dispatch_row_fft(int N, const RowFftArgs& r, int n_pol, hipStream_t s);
+
+}  // namespace pfb

@@ -16,14 +16,17 @@ struct AnalysisArgs {
   int64_t n_dat;
   float2* out;             // [pol][k][c]
   int64_t out_pol_stride;
-  int64_t K;               // output rows per pol
+  int64_t row0;            // first output row of this launch (global row index)
+  int64_t K;               // end of this launch's rows (exclusive, global)
+  int64_t K_total;         // output rows per pol of the whole call (padded circular shift)
   int n_pol;
   int N, M, P, nu, sds;    // channels, step, phases, os numerator, padded delay shift
   int variant;
   const float* taps;       // P*N padded taps (device)
   const float2* twN;       // e^{-2 pi i m / N}, m < N (device)
-  float2* scratch;         // generic path: [pol][K][N] (device) or null
-  int strips;              // fused kernel: persistent workgroups per pol (0 = auto)
+  float2* scratch;         // generic path: [pol][K - row0][N] (device) or null
+  int timing_mask;         // timing experiments only (PFB_ANA_MASK, results invalid): bit0 no
+                           // input loads, bit1 no FIR, bit2 no FFT, bit3 no output stores
 };
 
 // Synthesis stage 1: per channelised time row, N-point inverse DFT across channels

@@ -1,0 +1,59 @@
+// pfb_rowfft.hip — N-point row FFT launchers (row_fft_kernel, pfb_common.hpp): the
+// analysis FFT for N > 256 and synthesis stage 1 (the N-point inverse DFT across channels
+// of every channelised row, polyphase_synthesis.m:282-285 factored).
+#include "pfb_common.hpp"
+
+namespace pfb {
+
+template <int N, int DIR, bool PERM, bool GAIN>
+static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s) {
+  constexpr int ROWS = RowShape<N>::ROWS;
+  const size_t bytes = ((size_t)ROWS * RowShape<N>::RS + N) * sizeof(float2);
+  auto kern = row_fft_kernel<N, DIR, PERM, GAIN>;
+  hipError_t e = set_lds(kern, bytes);
+  if (e != hipSuccess) return e;
+  dim3 grid((unsigned)((r.n_rows + ROWS - 1) / ROWS), (unsigned)n_pol);
+  hipLaunchKernelGGL(kern, grid, dim3(NT), bytes, s, r);
+  return hipGetLastError();
+}
+
+template <int N, int DIR>
+static hipError_t launch_row_fft(const RowFftArgs& r, int n_pol, hipStream_t s) {
+  if constexpr (DIR > 0) {
+    if (r.perm && r.cgain) return launch_row_fft_t<N, DIR, true, true>(r, n_pol, s);
+    if (r.perm) return launch_row_fft_t<N, DIR, true, false>(r, n_pol, s);
+    if (r.cgain) return launch_row_fft_t<N, DIR, false, true>(r, n_pol, s);
+  }
+  return launch_row_fft_t<N, DIR, false, false>(r, n_pol, s);
+}
+
+template <int DIR>
+hipError_t dispatch_row_fft(int N, const RowFftArgs& r, int n_pol, hipStream_t s) {
+  switch (N) {
+    case 8: return launch_row_fft<8, DIR>(r, n_pol, s);
+    case 16: return launch_row_fft<16, DIR>(r, n_pol, s);
+    case 32: return launch_row_fft<32, DIR>(r, n_pol, s);
+    case 64: return launch_row_fft<64, DIR>(r, n_pol, s);
+    case 128: return launch_row_fft<128, DIR>(r, n_pol, s);
+    case 256: return launch_row_fft<256, DIR>(r, n_pol, s);
+    case 512: return launch_row_fft<512, DIR>(r, n_pol, s);
+    case 1024: return launch_row_fft<1024, DIR>(r, n_pol, s);
+    case 2048: return launch_row_fft<2048, DIR>(r, n_pol, s);
+    case 4096: return launch_row_fft<4096, DIR>(r, n_pol, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template hipError_t dispatch_row_fft<-1>(int, const RowFftArgs&, int, hipStream_t);
+template hipError_t dispatch_row_fft<+1>(int, const RowFftArgs&, int, hipStream_t);
+
+bool chan_ifft_supported(int N) { return pow2_supported(N); }
+
+hipError_t launch_chan_ifft(const ChanIfftArgs& c, hipStream_t s) {
+  if (c.n_rows <= 0) return hipSuccess;
+  RowFftArgs r{c.in, c.in_pol_stride, c.out, c.out_pol_stride, c.n_rows, c.perm, c.cgain, c.twN,
+               1.0f, 0, 0, 0, c.n_rows};
+  return dispatch_row_fft<+1>(c.N, r, c.n_pol, s);
+}
+
+}  // namespace pfb

@@ -10,7 +10,7 @@ kernels of ``lib/libpfb_hip.so`` (C ABI: ``include/pfb_api.h``).
 from ._lib import PfbError, device_count
 from .config import Rational, default_config, load_config
 from .core import (AnalysisPlan, SynthesisPlan, polyphase_analysis, polyphase_analysis_padded,
-                   polyphase_synthesis)
+                   polyphase_synthesis, roundtrip)
 from .filterbank import (Channelizer, DeChannelizer, FilterBank, InverseFilterBank,
                          TwoStageFilterBank, TwoStageInverseFilterBank)
 from .firio import (design_PFB_FIR_filter, design_PFB_FIR_filter_two_stage,
@@ -23,5 +23,5 @@ __all__ = [
     "SynthesisPlan", "polyphase_analysis", "polyphase_analysis_padded", "polyphase_synthesis",
     "Channelizer", "DeChannelizer", "FilterBank", "InverseFilterBank", "TwoStageFilterBank",
     "TwoStageInverseFilterBank", "design_PFB_FIR_filter", "design_PFB_FIR_filter_two_stage",
-    "read_fir_filter_coeff", "PFBWindow", "identity_taper",
+    "read_fir_filter_coeff", "PFBWindow", "identity_taper", "roundtrip",
 ]

@@ -87,6 +87,9 @@ SYMBOLS = [
     ("pfb_inverse_filterbank_buffered", c_int64, [c_void_p]),
     ("pfb_inverse_filterbank_reset", c_int32, [c_void_p]),
     ("pfb_synthesis_set_chunk_blocks", c_int32, [c_void_p, c_int32]),
+    ("pfb_roundtrip_execute", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64,
+                                        c_void_p, c_int64, c_int64, POINTER(c_int64), c_int64,
+                                        c_void_p, c_int64, c_int64, POINTER(c_int64), c_void_p]),
     ("pfb_last_error", c_char_p, []),
     ("pfb_api_version", c_int32, []),
     ("pfb_device_count", c_int32, []),

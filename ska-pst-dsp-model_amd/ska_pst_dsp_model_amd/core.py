@@ -28,7 +28,8 @@ from .config import Rational, as_rational
 from .window import PFBWindow, Taper, identity_taper
 
 __all__ = ["AnalysisPlan", "SynthesisPlan", "polyphase_analysis", "polyphase_analysis_padded",
-           "polyphase_synthesis", "analysis_plan", "synthesis_plan", "is_device_array"]
+           "polyphase_synthesis", "analysis_plan", "synthesis_plan", "is_device_array",
+           "roundtrip"]
 
 
 def _torch():
@@ -300,6 +301,41 @@ class SynthesisPlan:
                 self._h, src, n_dat * self.n_chan, n_dat, int(sample_offset), dst, cap, cap,
                 byref(n_out), mem, stream))
         return out[:, :n_out.value]
+
+
+# ============================================================================ round trip
+def roundtrip(analysis: AnalysisPlan, synthesis: SynthesisPlan, x, sample_offset: int = 1,
+              chan=None, out=None):
+    """Analysis -> synthesis of ``x`` (device tensor, (n_pol, n_dat) or (n_pol, 1, n_dat))
+    through ``pfb_roundtrip_execute`` — the sequence of test_data_pipeline.m:114,132.
+
+    Returns ``(chan, out)``: the full channelised product as a (n_pol, K, n_chan)
+    time-major buffer and the (n_pol, n_out) synthesised series.  Bit-identical to
+    ``analysis.execute(x)`` followed by ``synthesis.execute(chan, sample_offset,
+    layout="ptc")``; the library pipelines the two internally (include/pfb_api.h).
+    ``chan``/``out`` may be preallocated buffers of the right shapes (graph capture).
+    """
+    x, dev = analysis._prep_in(x)
+    if not dev:
+        raise ValueError("roundtrip() takes device tensors (use the separate calls for host arrays)")
+    t = _torch()
+    n_pol, n_dat = x.shape
+    if n_pol != analysis.n_pol or n_pol != synthesis.n_pol:
+        raise ValueError(f"plans built for n_pol={analysis.n_pol}/{synthesis.n_pol}, got {n_pol}")
+    K = analysis.output_length(n_dat)
+    n_out = synthesis.output_length(max(K - (int(sample_offset) - 1), 0))
+    if chan is None:
+        chan = t.empty((n_pol, max(K, 0), analysis.n_chan), dtype=t.complex64, device=x.device)
+    if out is None:
+        out = t.empty((n_pol, max(n_out, 0)), dtype=t.complex64, device=x.device)
+    if tuple(chan.shape) != (n_pol, K, analysis.n_chan) or tuple(out.shape) != (n_pol, n_out):
+        raise ValueError("preallocated chan/out have the wrong shape")
+    kr, no = c_int64(0), c_int64(0)
+    _lib.check(_lib.load().pfb_roundtrip_execute(
+        analysis._h, synthesis._h, c_void_p(x.data_ptr()), n_dat, n_dat,
+        c_void_p(chan.data_ptr()), K * analysis.n_chan, K, byref(kr), int(sample_offset),
+        c_void_p(out.data_ptr()), max(n_out, 1), n_out, byref(no), _stream_of(x)))
+    return chan, out
 
 
 # ============================================================================ plan cache

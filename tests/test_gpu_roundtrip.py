@@ -1,0 +1,173 @@
+"""GPU tests of the pipelined round trip (pfb_roundtrip_execute) and full-size parity.
+
+* The pipelined analysis -> synthesis must be bit-identical to the two separate calls
+  (same kernels, same inputs per row and per block; only the launch order differs) —
+  for both analysis variants, several chunk sizes, sample offsets and polarisations.
+* At the BASELINE C2 size (2^24 samples, 256 ch, OS 8/7, 3073 taps, Nf 256, Ov 48,
+  tukey, deripple) the round trip is compared with the float64 oracle at the
+  reference's 1e-6 criterion (test_matlab_dspsr_pfb_inversion.py:35,151-152), and a
+  size-independent property (linearity of the whole round trip) is checked too.
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_pfb_close
+from oracle import pfb_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _pfb():
+    import ska_pst_dsp_model_amd as pfb
+    return pfb
+
+
+def _noise_t(torch, dev, shape, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    re = torch.randn(shape, device=dev, generator=g)
+    im = torch.randn(shape, device=dev, generator=g)
+    return (torch.complex(re, im) / np.sqrt(2.0)).to(torch.complex64).contiguous()
+
+
+CASES = [
+    # (N, os, taps/chan, Nf, Ov, variant, n_pol, n_dat, chunk_blocks, sample_offset)
+    (256, "8/7", 12, 256, 48, "polyphase_analysis", 1, 1 << 20, 0, 1),
+    (256, "8/7", 12, 256, 48, "polyphase_analysis", 2, 1 << 19, 1, 1),
+    (256, "8/7", 12, 256, 48, "polyphase_analysis", 1, 1 << 19, 7, 5),
+    (256, "8/7", 12, 256, 48, "polyphase_analysis_padded", 1, 1 << 19, 3, 1),
+    (256, "8/7", 12, 256, 48, "polyphase_analysis_padded", 2, 1 << 19, 0, 9),
+    (256, "4/3", 12, 256, 48, "polyphase_analysis", 1, 1 << 19, 5, 1),
+    (8, "8/7", 10, 128, 16, "polyphase_analysis", 2, 9000, 1, 1),
+    (8, "8/7", 10, 128, 16, "polyphase_analysis_padded", 1, 9000, 2, 3),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_roundtrip_bit_identical_to_separate_calls(gpu, case):
+    import torch
+    pfb = _pfb()
+    N, os_, tpc, nf, ov, variant, n_pol, n_dat, cb, so = case
+    taps = pfb.design_PFB_FIR_filter(N, os_, tpc)
+    x = _noise_t(torch, gpu, (n_pol, n_dat), 7)
+    ana = pfb.AnalysisPlan(taps, N, os_, variant, n_pol, 0)
+    win = pfb.PFBWindow().lookup["tukey"](nf, ov)
+    syn = pfb.SynthesisPlan(N, os_, nf, ov, True, 1, True, taps, win, None, n_pol, 0)
+    chan_ref = ana.execute(x)
+    out_ref = syn.execute(chan_ref, sample_offset=so, layout="ptc")
+    if cb:
+        syn.set_chunk_blocks(cb)
+    chan, out = pfb.roundtrip(ana, syn, x, sample_offset=so)
+    torch.cuda.synchronize()
+    assert chan.shape == chan_ref.shape and out.shape == out_ref.shape
+    assert out.shape[1] > 0
+    assert torch.equal(chan, chan_ref), "channelised product differs"
+    assert torch.equal(out, out_ref), "synthesised output differs"
+
+
+def test_roundtrip_no_blocks_only_analysis(gpu):
+    """Too short for one synthesis block: the channelised product is still produced."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
+    n_dat = 3328 + 224 * 50
+    x = _noise_t(torch, gpu, (1, n_dat), 3)
+    ana = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
+    win = pfb.PFBWindow().lookup["tukey"](256, 48)
+    syn = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, 1, 0)
+    chan, out = pfb.roundtrip(ana, syn, x)
+    assert out.shape == (1, 0)
+    assert torch.equal(chan, ana.execute(x))
+
+
+def test_roundtrip_rejects_mismatched_plans(gpu):
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
+    x = _noise_t(torch, gpu, (1, 1 << 16), 3)
+    ana = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
+    win = pfb.PFBWindow().lookup["tukey"](128, 16)
+    t8 = pfb.design_PFB_FIR_filter(8, "8/7", 10)
+    syn = pfb.SynthesisPlan(8, "8/7", 128, 16, True, 1, True, t8, win, None, 1, 0)
+    with pytest.raises(pfb.PfbError):
+        pfb.roundtrip(ana, syn, x)
+
+
+def test_roundtrip_graph_capture(gpu):
+    """The pipelined step (two streams) replays correctly from a HIP graph."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
+    x = _noise_t(torch, gpu, (1, 1 << 19), 11)
+    ana = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
+    win = pfb.PFBWindow().lookup["tukey"](256, 48)
+    syn = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, 1, 0)
+    syn.set_chunk_blocks(4)
+    chan_ref = ana.execute(x)
+    out_ref = syn.execute(chan_ref, layout="ptc")
+    chan = torch.empty_like(chan_ref)
+    out = torch.empty_like(out_ref)
+    pfb.roundtrip(ana, syn, x, chan=chan, out=out)  # warm-up (allocates plan buffers)
+    torch.cuda.synchronize()
+    chan.zero_()
+    out.zero_()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            pfb.roundtrip(ana, syn, x, chan=chan, out=out)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(chan, chan_ref)
+    assert torch.equal(out, out_ref)
+
+
+# ------------------------------------------------------------------ BASELINE C2 size
+@pytest.fixture(scope="module")
+def c2(gpu):
+    """C2 round trip on 2^24 noise samples (seed 0), device and oracle results."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
+    assert len(taps) == 3073
+    n = 1 << 24
+    rng = np.random.default_rng(0)
+    x = ((rng.standard_normal((1, 1, n)) + 1j * rng.standard_normal((1, 1, n))) /
+         np.sqrt(2)).astype(np.complex64)
+    ana = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
+    win = pfb.PFBWindow().lookup["tukey"](256, 48)
+    syn = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, 1, 0)
+    xd = torch.from_numpy(x[:, 0, :]).to(gpu)
+    chan, out = pfb.roundtrip(ana, syn, xd)
+    torch.cuda.synchronize()
+    return dict(pfb=pfb, taps=taps, x=x, xd=xd, ana=ana, syn=syn,
+                chan=chan.cpu().numpy(), out=out.cpu().numpy())
+
+
+def test_c2_full_size_matches_oracle(c2):
+    """BASELINE configs[1] at full size: channelised data and output vs the oracle."""
+    taps, x = c2["taps"], c2["x"]
+    ref_chan = orc.polyphase_analysis(x, taps, 256, "8/7")       # (1, 256, K) float64 maths
+    assert_pfb_close(c2["chan"].transpose(0, 2, 1), ref_chan, what="C2 analysis")
+    win = orc.pfb_window("tukey", 256, 48)
+    ref = orc.polyphase_synthesis(ref_chan, 1, 256, "8/7",
+                                  {"apply_deripple": 1, "filter_coeff": taps}, 1, 48, win)
+    assert c2["out"].shape == (1, 16737280)
+    assert_pfb_close(c2["out"][:, None, :], ref, what="C2 round trip")
+
+
+def test_c2_full_size_linearity(c2):
+    """Size-independent property: RT(a x1 + b x2) = a RT(x1) + b RT(x2)."""
+    import torch
+    pfb = _pfb()
+    x1 = c2["xd"]
+    x2 = torch.roll(x1, 12345, dims=1).contiguous()
+    a, b = 0.75, -1.25j
+    _, y1 = pfb.roundtrip(c2["ana"], c2["syn"], x1)
+    _, y2 = pfb.roundtrip(c2["ana"], c2["syn"], x2)
+    _, y = pfb.roundtrip(c2["ana"], c2["syn"], (a * x1 + b * x2).to(torch.complex64))
+    lhs = y.cpu().numpy()
+    rhs = (a * y1 + b * y2).cpu().numpy()
+    assert_pfb_close(lhs, rhs, tol=2e-6, what="linearity")
