@@ -46,9 +46,11 @@ def parse():
     ap.add_argument("--chunk-blocks", type=int, default=0)
     ap.add_argument("--graph", type=int, default=1,
                     help="capture one step (3 kernel launches) in a HIP graph and replay it")
-    ap.add_argument("--pipeline", type=int, default=0,
-                    help="run the step through pfb_roundtrip_execute (analysis of chunk c+1 "
-                         "on a second stream beside the synthesis of chunk c); 0 = two calls")
+    ap.add_argument("--roundtrip", type=int, default=1,
+                    help="1: one pfb_roundtrip_execute call per step (the analysis kernel also "
+                         "runs the synthesis channel IFFT on the rows it produces; the "
+                         "channelised product is still written in full); 0: separate "
+                         "analysis and synthesis calls")
     ap.add_argument("--kernel-events", type=int, default=1,
                     help="record HIP events around every kernel in the timed region")
     return ap.parse_args()
@@ -138,7 +140,7 @@ def main():
     def step_pipelined():
         return pfb.roundtrip(ana, syn, x, chan=chan_buf, out=out_buf)
 
-    step = step_pipelined if args.pipeline else step_serial
+    step = step_pipelined if args.roundtrip else step_serial
 
     lib = _lib.load()
     for _ in range(args.warmup):
@@ -181,18 +183,18 @@ def main():
     # profiled region: the same K steps with HIP events recorded around every kernel
     # launch on the library's launch stream (per-kernel durations for the roofline;
     # the events add inter-kernel gaps, so this region is not used for `value`).  The
-    # kernels run one at a time here (two separate calls, one stream): a kernel's
-    # event-bracketed duration is its own, not shared with a concurrent one.
+    # kernels of a step run one after another on one stream, so a kernel's
+    # event-bracketed duration is its own.
     lib.pfb_profile_reset()
     lib.pfb_profile_enable(args.kernel_events)
-    el_prof = timed(args.steps, step_serial)
+    el_prof = timed(args.steps, step)
     lib.pfb_profile_enable(0)
 
     # per-kernel-class event timings (on the library's launch stream)
     import ctypes
-    names = ["analysis_fused", "synth_chan_ifft", "synth_block"]
+    names = ["analysis", "synth_chan_ifft", "synth_block", "analysis+chan_ifft"]
     kern = {}
-    for w in range(3):
+    for w in range(4):
         ms, nl, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
         lib.pfb_profile_read(w, ctypes.byref(ms), ctypes.byref(nl), ctypes.byref(by))
         if nl.value:
@@ -236,7 +238,7 @@ def main():
                        "channelised_rows": K, "output_samples_per_unit": n_out,
                        "parallelism": f"{world} independent units, one per GPU (no collective)",
                        "hip_graph": bool(args.graph),
-                       "pipelined": bool(args.pipeline)},
+                       "roundtrip_call": bool(args.roundtrip)},
             "roofline": roof,
             "round_trip_hbm_frac": round(rt_gbs / HBM_PEAK_GBS, 4),
             "ms_per_step_with_kernel_events": round(el_prof / args.steps * 1e3, 4),

@@ -195,7 +195,8 @@ pfb_status pfb_stream_synchronize(void* stream);
 
 /* Kernel timing: average duration (ms) of the named kernel class over the launches
  * recorded since the last reset, measured with HIP events on the plan's stream.
- * which: 0 = analysis, 1 = synthesis channel-IFFT, 2 = synthesis block kernel. */
+ * which: 0 = analysis, 1 = synthesis channel-IFFT, 2 = synthesis block kernel,
+ *        3 = analysis fused with the synthesis channel IFFT (pfb_roundtrip_execute). */
 pfb_status pfb_profile_enable(int32_t enable);
 pfb_status pfb_profile_read(int32_t which, double* total_ms, int64_t* launches, double* bytes);
 pfb_status pfb_profile_reset(void);

@@ -131,9 +131,9 @@ __global__ __launch_bounds__(NT) void analysis_fused_kernel(AnalysisArgs a) {
       const int r = (int)((kg * M) % N);
       pos = (n + r) % N;
     } else {
-      const int b = (int)(kg % a.nu);
-      const int idx = (b == 0) ? 0 : (int)(((int64_t)(a.nu - b) * (N - M)) % N);
-      pos = (n - idx + N) % N;
+      // idx = ((nu - (kg mod nu)) (N - M)) mod N = (M kg) mod N, since nu M = de N
+      const int idx = (int)((kg * M) & (N - 1));
+      pos = (n - idx + N) & (N - 1);
     }
     rows.store(k, pos, u[e]);
   }
@@ -179,8 +179,11 @@ struct StreamShape {
   static constexpr size_t lds_bytes = (size_t)F_OFF * sizeof(float) + F_LEN * sizeof(float);
 };
 
-template <int N, int P, int NU, int DE>
-__global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
+// ZOUT (round trip): each step's channelised rows are also inverse-transformed across
+// channels in LDS and written as synthesis stage-1 rows (AnalysisArgs::z), so the
+// synthesis does not re-read them from HBM.
+template <int N, int P, int NU, int DE, bool ZOUT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void analysis_stream_kernel(AnalysisArgs a) {
   using SH = StreamShape<N, P, NU, DE>;
   constexpr int M = SH::M, PE = SH::PE, QS = SH::QS, T = SH::T, NEW = SH::NEW, WIN = SH::WIN;
   extern __shared__ __attribute__((aligned(16))) float2 smem[];
@@ -202,9 +205,10 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(xpol + row_first * N, nbytes);
   auto ld = [&](int r) {  // window row r (relative to row_first)
     const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (r * N + c) * 8, 0, 0);
-    return __builtin_bit_cast(float2, v);
+    return __builtin_bit_cast(v2f, v);
   };
-  float2 win[WIN];
+  // (re, im) as a packed pair: one v_pk_fma_f32 per complex x real tap MAC
+  v2f win[WIN];
 #pragma unroll
   for (int i = 0; i < WIN; ++i) win[i] = ld(i);
 
@@ -221,7 +225,7 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
   for (int64_t stp = st0; stp < st1; ++stp) {
     const int rel = (int)(stp - st0) * NEW;  // window row 0 of this step
     // prefetch the next step's new rows (consumed when the window slides)
-    float2 pf[NEW];
+    v2f pf[NEW];
     if (stp + 1 < st1) {
 #pragma unroll
       for (int i = 0; i < NEW; ++i) pf[i] = ld(rel + WIN + i);
@@ -229,10 +233,10 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
     __syncthreads();  // previous step's FFT has read its rows (first step: F staged)
     // all NU x QS rows accumulate together (tap-outer order): consecutive FMAs are
     // independent, so the 4-cycle FMA latency never stalls issue
-    float2 acc[NU][QS];
+    v2f acc[NU][QS];
     static_for<0, NU>([&](auto sv) {
 #pragma unroll
-      for (int qq = 0; qq < QS; ++qq) acc[decltype(sv)::value][qq] = make_float2(0.f, 0.f);
+      for (int qq = 0; qq < QS; ++qq) acc[decltype(sv)::value][qq] = v2f{0.f, 0.f};
     });
     static_for<0, PE>([&](auto mv) {
       constexpr int m = decltype(mv)::value;
@@ -247,9 +251,7 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
         constexpr int bs = (s * M) / N;
         static_for<0, QS>([&](auto qv) {
           constexpr int qq = decltype(qv)::value;
-          const float2 v = win[DE * qq + m + bs];
-          acc[s][qq].x = fmaf(gm[s], v.x, acc[s][qq].x);
-          acc[s][qq].y = fmaf(gm[s], v.y, acc[s][qq].y);
+          acc[s][qq] = __builtin_elementwise_fma(v2f{gm[s], gm[s]}, win[DE * qq + m + bs], acc[s][qq]);
         });
       });
     });
@@ -257,13 +259,20 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
       constexpr int s = decltype(sv)::value;
       static_for<0, QS>([&](auto qv) {
         constexpr int qq = decltype(qv)::value;
-        rows.store(qq * NU + s, c, acc[s][qq]);
+        rows.store(qq * NU + s, c, make_float2(acc[s][qq].x, acc[s][qq].y));
       });
     });
     __syncthreads();
     st.k0 = (q_lo + stp * QS) * NU;
     if (a.timing_mask & 8) st.K = 0;
-    if (a.timing_mask & 4) {
+    if constexpr (ZOUT) {
+      // analysis FFT -> HBM + LDS; then the synthesis channel IFFT -> Z (row_fft_kernel
+      // <N, +1>'s passes on the same values)
+      block_fft<N, -1, T, NT>(rows, AnalysisStoreKeep{st, rows}, rows, tw, c);
+      __syncthreads();
+      const ZStore zs{a.z + pol * a.z_pol_stride, st.k0, a.K, a.z_row0, N};
+      block_fft<N, +1, T, NT>(rows, zs, rows, tw, c);
+    } else if (a.timing_mask & 4) {
 #pragma unroll
       for (int r = 0; r < T; ++r) st.store(r, c, rows.load(r, c));
     } else {
@@ -326,7 +335,7 @@ static hipError_t launch_fused(const AnalysisArgs& a, hipStream_t s) {
 template <int N, int P, int NU, int DE>
 static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
   using SH = StreamShape<N, P, NU, DE>;
-  auto kern = analysis_stream_kernel<N, P, NU, DE>;
+  auto kern = a.z ? analysis_stream_kernel<N, P, NU, DE, true> : analysis_stream_kernel<N, P, NU, DE, false>;
   hipError_t e = set_lds(kern, SH::lds_bytes);
   if (e != hipSuccess) return e;
   const int64_t q_lo = a.row0 / NU;
@@ -377,8 +386,13 @@ bool analysis_supported(int N, int P, int variant, bool* fused) {
   return pow2_supported(N);
 }
 
+bool analysis_can_emit_z(const AnalysisArgs& a) {
+  return stream_shape(a) && std::getenv("PFB_ANALYSIS_NO_STREAM") == nullptr;
+}
+
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
   if (a.K <= a.row0) return hipSuccess;
+  if (a.z && !analysis_can_emit_z(a)) return hipErrorInvalidValue;
   bool fused = false;
   if (!analysis_supported(a.N, a.P, a.variant, &fused)) return hipErrorInvalidValue;
   static const bool no_stream = std::getenv("PFB_ANALYSIS_NO_STREAM") != nullptr;

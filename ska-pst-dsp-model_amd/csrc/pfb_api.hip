@@ -90,9 +90,9 @@ struct Profiler {
   bool enabled = false;
   std::vector<ProfRec> pending;
   std::vector<hipEvent_t> pool;
-  double total_ms[3] = {0, 0, 0};
-  int64_t launches[3] = {0, 0, 0};
-  double bytes[3] = {0, 0, 0};
+  double total_ms[4] = {0, 0, 0, 0};  // 0 analysis, 1 chan IFFT, 2 block, 3 analysis + chan IFFT
+  int64_t launches[4] = {0, 0, 0, 0};
+  double bytes[4] = {0, 0, 0, 0};
   hipEvent_t get() {
     if (!pool.empty()) {
       hipEvent_t e = pool.back();
@@ -161,11 +161,17 @@ struct pfb_analysis_plan {
 
 // Rows [row0, K_end) of a call whose output has K_total rows per pol (the padded
 // variant's circular shift is modulo K_total).  `in`/`out` are the call's bases.
+// z (round trip only): also emit the synthesis stage-1 rows of rows >= z_row0 into
+// z[pol][k - z_row0][t0] (AnalysisArgs::z).
 static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
                                float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
-                               int64_t K_total, hipStream_t s) {
+                               int64_t K_total, hipStream_t s, float2* z = nullptr,
+                               int64_t z_ps = 0, int64_t z_row0 = 0) {
   if (K_end <= row0) return PFB_OK;
   pfb::AnalysisArgs a{};
+  a.z = z;
+  a.z_pol_stride = z_ps;
+  a.z_row0 = z_row0;
   a.in = in;
   a.in_pol_stride = in_ps;
   a.n_dat = n_dat;
@@ -193,10 +199,21 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   const int64_t in_samples = (K_end == K_total && row0 == 0)
                                  ? n_dat
                                  : (K_end - row0) * p->M + (K_end == K_total ? n_dat - K_total * p->M : 0);
-  const double bytes = (double)p->n_pol * (8.0 * in_samples + 8.0 * (K_end - row0) * p->N);
-  ProfScope ps(0, bytes, s);
+  double bytes = (double)p->n_pol * (8.0 * in_samples + 8.0 * (K_end - row0) * p->N);
+  if (z) bytes += (double)p->n_pol * 8.0 * (K_end - std::max(row0, z_row0)) * p->N;  // + Z rows
+  ProfScope ps(z ? 3 : 0, bytes, s);
   HIPCHK(pfb::launch_analysis(a, s));
   return PFB_OK;
+}
+
+static bool analysis_emits_z(const pfb_analysis_plan* p) {
+  pfb::AnalysisArgs a{};
+  a.variant = p->variant;
+  a.N = p->N;
+  a.M = p->M;
+  a.P = p->P;
+  a.nu = p->nu;
+  return p->fused && pfb::analysis_can_emit_z(a);
 }
 
 static int64_t analysis_K(const pfb_analysis_plan* p, int64_t n_dat) {
@@ -408,6 +425,7 @@ struct pfb_synthesis_plan {
   int rt_chunk_blocks = 64;  // round-trip pipeline chunk (PFB_RT_CHUNK_BLOCKS)
   int timing_mask = 0;  // PFB_TIMING_MASK (timing experiments; results invalid when set)
   int ranges = -1;  // PFB_SYNTH_RANGES: 0 one workgroup per block, -1 persistent auto, >0 persistent
+  int no_reuse = 0;  // PFB_SYNTH_NO_REUSE: re-read the overlap rows (A/B measurement only)
   bool identity_perm = true;
   bool has_cgain = false;
   DevBuf window, tw4, twN, twNf, twW, perm, cgain;
@@ -428,6 +446,10 @@ static int64_t synth_blocks(const pfb_synthesis_plan* p, int64_t n_dat) {
   const int64_t b = floordiv(n_dat - 2 * (int64_t)p->Ov, p->keep);
   return std::max<int64_t>(b, 0);
 }
+
+static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64_t z_ps, int64_t b0,
+                                   int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
+                                   hipStream_t s);
 
 // Blocks [b0, b0 + nb) of a call: channel IFFT of their rows into Z, then the block
 // kernel.  `in` is the call's first channelised row (sample_offset applied).
@@ -452,9 +474,16 @@ static pfb_status synthesis_chunk(pfb_synthesis_plan* p, const float2* in, int64
     ProfScope ps(1, (double)p->n_pol * rows * p->N * 16.0, s);
     HIPCHK(pfb::launch_chan_ifft(c, s));
   }
+  return synthesis_blocks(p, Z, rows * p->N, b0, nb, out, out_ps, out_limit, s);
+}
+
+// Block kernel over blocks [b0, b0 + nb); Z row 0 is channelised row b0 * keep.
+static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64_t z_ps, int64_t b0,
+                                   int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
+                                   hipStream_t s) {
   pfb::SynthBlockArgs a{};
   a.Z = Z;
-  a.z_pol_stride = rows * p->N;
+  a.z_pol_stride = z_ps;
   a.out = out;
   a.out_pol_stride = out_ps;
   a.block0 = b0;
@@ -477,6 +506,7 @@ static pfb_status synthesis_chunk(pfb_synthesis_plan* p, const float2* in, int64
   a.twW = p->twW.as<float2>();
   a.out_limit = out_limit;
   a.ranges = p->ranges;
+  a.no_reuse = p->no_reuse;
   a.timing_mask = p->timing_mask;
   {
     ProfScope ps(2, (double)p->n_pol * (nb * p->keep * p->N * 8.0 + nb * p->Lkeep * 8.0), s);
@@ -546,6 +576,7 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
   p->device = d->device;
   if (const char* v = std::getenv("PFB_SYNTH_RANGES")) p->ranges = std::max(-1, std::atoi(v));
   if (const char* v = std::getenv("PFB_TIMING_MASK")) p->timing_mask = std::atoi(v);
+  if (const char* v = std::getenv("PFB_SYNTH_NO_REUSE")) p->no_reuse = std::atoi(v) != 0;
   if (const char* v = std::getenv("PFB_RT_CHUNK_BLOCKS")) p->rt_chunk_blocks = std::max(1, std::atoi(v));
   p->N = N;
   p->nu = nu;
@@ -862,6 +893,24 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
   float2* y = (float2*)chan;
   if (B == 0) return analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s);
 
+  // Fused: the analysis kernel also runs the synthesis channel IFFT on every row it
+  // produces (same arithmetic on the same float values, so the output is bit-identical
+  // to the separate calls) and the block kernel reads those rows — the channelised
+  // product is still written in full.  Needs the streaming analysis kernel, no combine
+  // permutation / per-channel gain, and scratch for all K - off rows (bounded at 2 GiB;
+  // an explicit chunk size keeps the chunked pipeline below).
+  static const bool no_fuse = std::getenv("PFB_RT_NO_FUSE") != nullptr;
+  const int64_t zrows = K - off;
+  const size_t zbytes = (size_t)pa->n_pol * zrows * pa->N * sizeof(float2);
+  if (!no_fuse && analysis_emits_z(pa) && ps->identity_perm && !ps->has_cgain &&
+      ps->chunk_blocks <= 0 && zbytes <= ((size_t)2 << 30)) {
+    HIPCHK(ps->Z.ensure(zbytes));
+    float2* Z = ps->Z.as<float2>();
+    pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, off);
+    if (st != PFB_OK) return st;
+    return synthesis_blocks(ps, Z, zrows * pa->N, 0, B, (float2*)out, out_ps, olen, s);
+  }
+
   if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));
   int64_t CB = ps->chunk_blocks > 0 ? ps->chunk_blocks : ps->rt_chunk_blocks;
   CB = std::max<int64_t>(1, std::min<int64_t>(CB, B));
@@ -930,7 +979,7 @@ pfb_status pfb_profile_enable(int32_t enable) {
   return PFB_OK;
 }
 pfb_status pfb_profile_read(int32_t which, double* total_ms, int64_t* launches, double* bytes) {
-  if (which < 0 || which > 2) return fail(PFB_ERR_INVALID_ARG, "which must be 0..2");
+  if (which < 0 || which > 3) return fail(PFB_ERR_INVALID_ARG, "which must be 0..3");
   g_prof.drain();
   if (total_ms) *total_ms = g_prof.total_ms[which];
   if (launches) *launches = g_prof.launches[which];
@@ -939,7 +988,7 @@ pfb_status pfb_profile_read(int32_t which, double* total_ms, int64_t* launches, 
 }
 pfb_status pfb_profile_reset(void) {
   g_prof.drain();
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < 4; ++i) {
     g_prof.total_ms[i] = 0;
     g_prof.launches[i] = 0;
     g_prof.bytes[i] = 0;

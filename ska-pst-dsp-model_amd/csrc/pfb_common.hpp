@@ -27,11 +27,41 @@ struct AnalysisStore {
     if (kg < K && kg >= k_lo) {
       int64_t t = kg;
       if (padded) {
-        t = (kg - sds) % Ktot;
-        if (t < 0) t += Ktot;
+        // circular -sds shift (polyphase_analysis_padded.m:156); 0 <= kg < Ktot, so one
+        // wrap suffices unless sds exceeds the row count (tiny inputs)
+        t = kg - sds;
+        while (t < 0) t += Ktot;
       }
       out[t * N + c] = cscale(v, scale);
     }
+  }
+};
+
+// Last pass of the analysis FFT in the round trip: the channelised row goes to HBM
+// (as AnalysisStore) AND back into the LDS rows, where the synthesis channel IFFT reads
+// it — the same float values row_fft_kernel would load from HBM.  kIsLds: the pass
+// places its barrier between its LDS loads and these in-place stores.
+struct AnalysisStoreKeep {
+  static constexpr bool kIsLds = true;
+  AnalysisStore hbm;
+  LdsIO lds;
+  __device__ __forceinline__ void store(int row, int c, float2 v) const {
+    const float2 y = cscale(v, hbm.scale);
+    const int64_t kg = hbm.k0 + row;
+    if (kg < hbm.K && kg >= hbm.k_lo) hbm.out[kg * hbm.N + c] = y;
+    lds.store(row, c, y);
+  }
+};
+
+// Synthesis stage-1 output row (Z) of analysis row k0 + row: Z row k - z_row0.
+struct ZStore {
+  static constexpr bool kIsLds = false;
+  float2* z;
+  int64_t k0, K, z_row0;
+  int N;
+  __device__ __forceinline__ void store(int row, int c, float2 v) const {
+    const int64_t kg = k0 + row;
+    if (kg < K && kg >= z_row0) z[(kg - z_row0) * N + c] = cscale(v, 1.0f);
   }
 };
 
@@ -68,9 +98,9 @@ struct RowStore {
     const int64_t r = r0 + row;
     if (r < n_rows) {
       int64_t t = row_base + r;
-      if (remap) {
-        t = (t - sds) % n_total;
-        if (t < 0) t += n_total;
+      if (remap) {  // row_base + r < n_total: one wrap (more only for tiny inputs)
+        t -= sds;
+        while (t < 0) t += n_total;
       }
       out[t * N + c] = cscale(v, scale);
     }

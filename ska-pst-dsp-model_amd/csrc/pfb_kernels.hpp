@@ -27,7 +27,15 @@ struct AnalysisArgs {
   float2* scratch;         // generic path: [pol][K - row0][N] (device) or null
   int timing_mask;         // timing experiments only (PFB_ANA_MASK, results invalid): bit0 no
                            // input loads, bit1 no FIR, bit2 no FFT, bit3 no output stores
+  // Round trip only (pfb_roundtrip_execute): when z is set, every output row k >= z_row0
+  // is also transformed by the synthesis stage-1 channel IFFT (the exact computation
+  // row_fft_kernel<N, +1> performs on the stored row) into z[pol][k - z_row0][t0].
+  float2* z;
+  int64_t z_pol_stride;
+  int64_t z_row0;
 };
+// analysis kernels that can also emit the synthesis stage-1 rows (see AnalysisArgs::z)
+bool analysis_can_emit_z(const AnalysisArgs& a);
 
 // Synthesis stage 1: per channelised time row, N-point inverse DFT across channels
 // (after the combine permutation and per-channel gain).  See DESIGN.md §synthesis.
@@ -64,6 +72,7 @@ struct SynthBlockArgs {
   const float2* twW;       // e^{-2 pi i m / W}
   int64_t out_limit;       // samples per pol actually written (InverseFilterBank trim)
   int ranges;              // 0: one workgroup per block; -1 persistent auto; >0 persistent ranges
+  int no_reuse;            // 1: re-read the 2 Ov overlap rows from HBM (PFB_SYNTH_NO_REUSE, A/B only)
   int timing_mask;         // timing experiments only (PFB_TIMING_MASK): bit0 drop Z loads,
                            // bit1 drop output stores, bit2 drop tw4 loads (results invalid)
 };

@@ -133,6 +133,17 @@ template <> struct SynthPlan<128, 96> : FusedPlan<8, Radices<>, 16, Radices<8>> 
 template <> struct SynthPlan<512, 448> : FusedPlan<8, Radices<4>, 16, Radices<8, 4>> {};
 template <> struct SynthPlan<1024, 896> : FusedPlan<16, Radices<4>, 16, Radices<8, 8>> {};
 
+// Overlap-reuse instance per transform size: DK = keep / (NF / R1) for the configured
+// overlap (SKA-Low Nf 256 / Ov 48: keep 160; 'test' Nf 128 / Ov 16: keep 96; SKA-Mid
+// Nf 512 / Ov 128: keep 256).  Other overlaps run the plain persistent instance.
+template <int NF, int W>
+constexpr int synth_reuse_dk() {
+  if constexpr (NF == 256) return 10;
+  else if constexpr (NF == 128) return 6;
+  else if constexpr (NF == 512) return 4;
+  else return 0;
+}
+
 template <int NF, int W>
 constexpr int synth_first_radix() {
   if constexpr (SynthPlan<NF, W>::fused) return SynthPlan<NF, W>::R1;
@@ -205,8 +216,12 @@ __device__ __forceinline__ void fused_select_pass(const LdsPairs& rowsF, const L
 
 // PERSIST: workgroup (tg, rr) walks a range of blocks and prefetches the next one's
 // first-pass inputs into registers while it transforms the current one.
-template <int NF, int W, int PAIRS, bool SPANS, bool PERSIST>
-__global__ __launch_bounds__(NTP) void synth_block_kernel(SynthBlockArgs a) {
+// DK > 0 (keep = DK * NF / R1): consecutive blocks overlap by 2 Ov = NF - keep rows, and
+// first-pass register r of a thread holds row j + r NF/R1 — so the next block's
+// registers 0 .. R1-DK-1 are this block's registers DK .. R1-1: they move in registers
+// and only DK of the R1 rows are read from HBM (the 2 Ov overlap re-read disappears).
+template <int NF, int W, int PAIRS, bool SPANS, bool PERSIST, int DK = 0>
+__global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void synth_block_kernel(SynthBlockArgs a) {
   using SS = SynthPairShape<NF, W, PAIRS>;
   using SP = SynthPlan<NF, W>;
   constexpr int R1 = synth_first_radix<NF, W>();
@@ -289,24 +304,27 @@ __global__ __launch_bounds__(NTP) void synth_block_kernel(SynthBlockArgs a) {
     } else {
       constexpr int PF = (PAIRS * NB1 + NTP - 1) / NTP;
       cpx2 zv[PF][R1];
-      auto prefetch = [&](int b) {
+      static_assert(DK >= 0 && DK <= R1, "overlap reuse needs keep = DK * NF / R1");
+      auto prefetch = [&](int b, auto reuse) {
+        constexpr int R0 = decltype(reuse)::value ? R1 - DK : 0;  // registers kept
         const __amdgpu_buffer_rsrc_t z = make_rsrc(zpol + (int64_t)b * a.keep * N, zbytes);
         static_for<0, PF>([&](auto p) {
           const int bb = min(tid + p * NTP, PAIRS * NB1 - 1);
           const int q = bb % PAIRS, j = bb / PAIRS;
-          static_for<0, R1>([&](auto r) {
+          static_for<0, R0>([&](auto r) { zv[p][r] = zv[p][r + DK]; });
+          static_for<R0, R1>([&](auto r) {
             const v4u x = __builtin_amdgcn_raw_buffer_load_b128(z, (j * N + 2 * q) * 8, r * NB1 * N * 8, 0);
             zv[p][r] = from_interleaved(__builtin_bit_cast(v4f, x));
           });
         });
       };
-      prefetch(b_begin);
+      prefetch(b_begin, std::false_type{});
       const PairRegsIn<PF, R1> in{zv, win};
 #pragma unroll 1
       for (int b = b_begin; b < b_end; b += b_step) {
         __syncthreads();  // tables / previous block's W transform done with the rows
         run_block(in, b, [&] {
-          if (b + b_step < b_end) prefetch(b + b_step);
+          if (b + b_step < b_end) prefetch(b + b_step, std::integral_constant<bool, (DK > 0)>{});
         });
       }
     }
@@ -318,8 +336,13 @@ static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
   using SS = SynthPairShape<NF, W, PAIRS>;
   const int groups = a.N / (2 * PAIRS);
   if (a.ranges != 0 && SynthPlan<NF, W>::fused) {
-    // persistent: block ranges so that ~LDS-limited workgroups per CU are resident
-    auto kern = synth_block_kernel<NF, W, PAIRS, SPANS, SynthPlan<NF, W>::fused>;
+    // persistent: block ranges so that ~LDS-limited workgroups per CU are resident;
+    // the overlap-reuse instance when keep matches the compiled DK
+    constexpr int NB1 = NF / synth_first_radix<NF, W>();
+    constexpr int DK = synth_reuse_dk<NF, W>();
+    auto kern = (DK > 0 && a.keep == DK * NB1 && !a.no_reuse)
+                    ? synth_block_kernel<NF, W, PAIRS, SPANS, SynthPlan<NF, W>::fused, DK>
+                    : synth_block_kernel<NF, W, PAIRS, SPANS, SynthPlan<NF, W>::fused, 0>;
     hipError_t e = set_lds(kern, SS::lds_bytes);
     if (e != hipSuccess) return e;
     const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / SS::lds_bytes));

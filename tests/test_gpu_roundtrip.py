@@ -37,6 +37,10 @@ CASES = [
     (256, "8/7", 12, 256, 48, "polyphase_analysis_padded", 1, 1 << 19, 3, 1),
     (256, "8/7", 12, 256, 48, "polyphase_analysis_padded", 2, 1 << 19, 0, 9),
     (256, "4/3", 12, 256, 48, "polyphase_analysis", 1, 1 << 19, 5, 1),
+    # chunk 0 with the streaming analysis shapes = the fused path (analysis kernel
+    # emits the synthesis stage-1 rows)
+    (256, "4/3", 12, 256, 48, "polyphase_analysis", 2, 1 << 19, 0, 3),
+    (256, "8/7", 11, 256, 48, "polyphase_analysis", 1, (1 << 19) + 777, 0, 2),
     (8, "8/7", 10, 128, 16, "polyphase_analysis", 2, 9000, 1, 1),
     (8, "8/7", 10, 128, 16, "polyphase_analysis_padded", 1, 9000, 2, 3),
 ]
@@ -92,8 +96,10 @@ def test_roundtrip_rejects_mismatched_plans(gpu):
         pfb.roundtrip(ana, syn, x)
 
 
-def test_roundtrip_graph_capture(gpu):
-    """The pipelined step (two streams) replays correctly from a HIP graph."""
+@pytest.mark.parametrize("chunk_blocks", [4, 0])
+def test_roundtrip_graph_capture(gpu, chunk_blocks):
+    """The round-trip step replays correctly from a HIP graph: the pipelined form (two
+    streams, chunk 4) and the fused form (chunk 0: one stream, analysis emits Z)."""
     import torch
     pfb = _pfb()
     taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
@@ -101,9 +107,10 @@ def test_roundtrip_graph_capture(gpu):
     ana = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
     win = pfb.PFBWindow().lookup["tukey"](256, 48)
     syn = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, 1, 0)
-    syn.set_chunk_blocks(4)
     chan_ref = ana.execute(x)
     out_ref = syn.execute(chan_ref, layout="ptc")
+    if chunk_blocks:
+        syn.set_chunk_blocks(chunk_blocks)
     chan = torch.empty_like(chan_ref)
     out = torch.empty_like(out_ref)
     pfb.roundtrip(ana, syn, x, chan=chan, out=out)  # warm-up (allocates plan buffers)
