@@ -183,7 +183,7 @@ struct StreamShape {
 // channels in LDS and written as synthesis stage-1 rows (AnalysisArgs::z), so the
 // synthesis does not re-read them from HBM.
 template <int N, int P, int NU, int DE, bool ZOUT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void analysis_stream_kernel(AnalysisArgs a) {
+__global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
   using SH = StreamShape<N, P, NU, DE>;
   constexpr int M = SH::M, PE = SH::PE, QS = SH::QS, T = SH::T, NEW = SH::NEW, WIN = SH::WIN;
   extern __shared__ __attribute__((aligned(16))) float2 smem[];
@@ -218,18 +218,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void an
 #pragma unroll
   for (int m = 0; m < P + 2; ++m) F[m * N + c] = (m >= 1 && m <= P) ? a.taps[(m - 1) * N + c] : 0.f;
 
-  AnalysisStore st{a.out + pol * a.out_pol_stride, a.K, a.K_total, 0, N, a.sds, 0, (float)N, a.row0};
+  float2* opol = a.out + pol * a.out_pol_stride;
+  float2* zpol = ZOUT ? a.z + pol * a.z_pol_stride - a.z_row0 * N : nullptr;  // Z row k - z_row0
   LdsRows rows(smem, SH::RS);
   const float2* tw = smem + SH::TW_OFF;
 #pragma unroll 1
   for (int64_t stp = st0; stp < st1; ++stp) {
     const int rel = (int)(stp - st0) * NEW;  // window row 0 of this step
     // prefetch the next step's new rows (consumed when the window slides)
+    // (unconditional: past the range it reads rows nobody uses, or zeros past n_dat —
+    // a conditional prefetch makes vmcnt path-dependent and the next step waits for
+    // every store as well)
     v2f pf[NEW];
-    if (stp + 1 < st1) {
 #pragma unroll
-      for (int i = 0; i < NEW; ++i) pf[i] = ld(rel + WIN + i);
-    }
+    for (int i = 0; i < NEW; ++i) pf[i] = ld(rel + WIN + i);
     __syncthreads();  // previous step's FFT has read its rows (first step: F staged)
     // all NU x QS rows accumulate together (tap-outer order): consecutive FMAs are
     // independent, so the 4-cycle FMA latency never stalls issue
@@ -245,7 +247,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void an
         constexpr int s = decltype(sv)::value;
         gm[s] = F[(m + 1) * N + c - (s * M) % N];
       });
-      if ((a.timing_mask & 2) && m > 0) return;
       static_for<0, NU>([&](auto sv) {
         constexpr int s = decltype(sv)::value;
         constexpr int bs = (s * M) / N;
@@ -263,18 +264,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void an
       });
     });
     __syncthreads();
-    st.k0 = (q_lo + stp * QS) * NU;
-    if (a.timing_mask & 8) st.K = 0;
+    const int64_t k0 = (q_lo + stp * QS) * NU;
+    const BufRowStore st = BufRowStore::rows(opol, k0, T, a.row0, a.K, N, (float)N);
     if constexpr (ZOUT) {
       // analysis FFT -> HBM + LDS; then the synthesis channel IFFT -> Z (row_fft_kernel
       // <N, +1>'s passes on the same values)
-      block_fft<N, -1, T, NT>(rows, AnalysisStoreKeep{st, rows}, rows, tw, c);
+      block_fft<N, -1, T, NT>(rows, BufStoreKeep{st, rows}, rows, tw, c);
       __syncthreads();
-      const ZStore zs{a.z + pol * a.z_pol_stride, st.k0, a.K, a.z_row0, N};
+      const BufRowStore zs = BufRowStore::rows(zpol, k0, T, max(a.row0, a.z_row0), a.K, N, 1.0f);
       block_fft<N, +1, T, NT>(rows, zs, rows, tw, c);
-    } else if (a.timing_mask & 4) {
-#pragma unroll
-      for (int r = 0; r < T; ++r) st.store(r, c, rows.load(r, c));
     } else {
       block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
     }

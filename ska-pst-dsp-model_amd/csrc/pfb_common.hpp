@@ -37,31 +37,39 @@ struct AnalysisStore {
   }
 };
 
-// Last pass of the analysis FFT in the round trip: the channelised row goes to HBM
-// (as AnalysisStore) AND back into the LDS rows, where the synthesis channel IFFT reads
-// it — the same float values row_fft_kernel would load from HBM.  kIsLds: the pass
-// places its barrier between its LDS loads and these in-place stores.
-struct AnalysisStoreKeep {
-  static constexpr bool kIsLds = true;
-  AnalysisStore hbm;
-  LdsIO lds;
+// Row store through a range-checked buffer descriptor: rows [lo, records / (8 N)) of
+// the descriptor's base are written, others dropped by the hardware (an out-of-range
+// offset) — no branch per store, so the wave's vmcnt count stays path-independent and
+// a later wait for a prefetch never has to wait for these stores too.
+struct BufRowStore {
+  static constexpr bool kIsLds = false;
+  __amdgpu_buffer_rsrc_t r;
+  int lo, N;
+  float scale;
   __device__ __forceinline__ void store(int row, int c, float2 v) const {
-    const float2 y = cscale(v, hbm.scale);
-    const int64_t kg = hbm.k0 + row;
-    if (kg < hbm.K && kg >= hbm.k_lo) hbm.out[kg * hbm.N + c] = y;
-    lds.store(row, c, y);
+    const uint32_t off = row >= lo ? (uint32_t)((row * N + c) * 8) : 0xFFFFFFF0u;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v, scale)), r, off, 0, 0);
+  }
+  // rows [k0, k0 + T) of a [row][N] array at `base`, valid rows [k_lo, k_hi)
+  __device__ __forceinline__ static BufRowStore rows(float2* base, int64_t k0, int T, int64_t k_lo,
+                                                      int64_t k_hi, int N, float scale) {
+    const int64_t hi = min(max(k_hi - k0, (int64_t)0), (int64_t)T);
+    const int lo = (int)min(max(k_lo - k0, (int64_t)0), (int64_t)T);
+    return BufRowStore{make_rsrc(base + k0 * N, (uint32_t)(hi * N * 8)), lo, N, scale};
   }
 };
 
-// Synthesis stage-1 output row (Z) of analysis row k0 + row: Z row k - z_row0.
-struct ZStore {
-  static constexpr bool kIsLds = false;
-  float2* z;
-  int64_t k0, K, z_row0;
-  int N;
+// The analysis FFT's last pass in the round trip, branch-free (BufRowStore): the row
+// goes to HBM and back into the LDS rows for the synthesis channel IFFT.
+struct BufStoreKeep {
+  static constexpr bool kIsLds = true;
+  BufRowStore hbm;
+  LdsIO lds;
   __device__ __forceinline__ void store(int row, int c, float2 v) const {
-    const int64_t kg = k0 + row;
-    if (kg < K && kg >= z_row0) z[(kg - z_row0) * N + c] = cscale(v, 1.0f);
+    const float2 y = cscale(v, hbm.scale);
+    const uint32_t off = row >= hbm.lo ? (uint32_t)((row * hbm.N + c) * 8) : 0xFFFFFFF0u;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y), hbm.r, off, 0, 0);
+    lds.store(row, c, y);
   }
 };
 

@@ -26,7 +26,7 @@ struct AnalysisArgs {
   const float2* twN;       // e^{-2 pi i m / N}, m < N (device)
   float2* scratch;         // generic path: [pol][K - row0][N] (device) or null
   int timing_mask;         // timing experiments only (PFB_ANA_MASK, results invalid): bit0 no
-                           // input loads, bit1 no FIR, bit2 no FFT, bit3 no output stores
+                           // input loads (streaming kernel)
   // Round trip only (pfb_roundtrip_execute): when z is set, every output row k >= z_row0
   // is also transformed by the synthesis stage-1 channel IFFT (the exact computation
   // row_fft_kernel<N, +1> performs on the stored row) into z[pol][k - z_row0][t0].

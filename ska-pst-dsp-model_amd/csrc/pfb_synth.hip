@@ -61,15 +61,17 @@ struct PairZIn {
   }
 };
 
-// first Nf-point pass input from prefetched registers
+// first Nf-point pass input from prefetched registers, kept in memory order until used:
+// from_interleaved's v_swap_b32 is inline asm, so converting at load time would make
+// the wave wait for the HBM prefetch right after issuing it
 template <int PER, int R>
 struct PairRegsIn {
   static constexpr bool kIsLds = false;
-  const cpx2 (&zv)[PER][R];
+  const v4f (&zv)[PER][R];
   const float* win;
   template <class P, class RR>
   __device__ __forceinline__ cpx2 load(int, int tau, P, RR) const {
-    return cscale(zv[P::value][RR::value], win[tau]);
+    return cscale(from_interleaved(zv[P::value][RR::value]), win[tau]);
   }
 };
 
@@ -160,8 +162,9 @@ constexpr int fused_src(int rr) {
 
 // gain x four-step twiddle of the fused pass inputs: slot r'' of pair row q, butterfly j
 // is bin j' = j + NBL r'' ([j'][t0] table, 16-byte loads, all unconditional)
+// (memory order; converted where the fused pass uses them, see PairRegsIn)
 template <int NBL, int RW1, int PAIRS, int NTH>
-__device__ __forceinline__ void load_t4(cpx2 (&t4)[(PAIRS * NBL + NTH - 1) / NTH][RW1],
+__device__ __forceinline__ void load_t4(v4f (&t4)[(PAIRS * NBL + NTH - 1) / NTH][RW1],
                                         __amdgpu_buffer_rsrc_t tr, int N, int tid) {
   constexpr int TOT = PAIRS * NBL;
   static_for<0, (TOT + NTH - 1) / NTH>([&](auto p) {
@@ -169,7 +172,7 @@ __device__ __forceinline__ void load_t4(cpx2 (&t4)[(PAIRS * NBL + NTH - 1) / NTH
     const int q = b % PAIRS, j = b / PAIRS;
     static_for<0, RW1>([&](auto rr) {
       const v4u x = __builtin_amdgcn_raw_buffer_load_b128(tr, ((j + NBL * rr) * N + 2 * q) * 8, 0, 0);
-      t4[p][rr] = from_interleaved(__builtin_bit_cast(v4f, x));
+      t4[p][rr] = __builtin_bit_cast(v4f, x);
     });
   });
 }
@@ -180,8 +183,8 @@ __device__ __forceinline__ void load_t4(cpx2 (&t4)[(PAIRS * NBL + NTH - 1) / NTH
 template <int NF, int W, int RL, bool SPANS, int PAIRS, int NTH>
 __device__ __forceinline__ void fused_select_pass(const LdsPairs& rowsF, const LdsPairs& rowsW,
                                                   const float2* __restrict__ twF,
-                                                  const cpx2 (&t4)[(PAIRS * (NF / RL) + NTH - 1) / NTH]
-                                                                  [W / (NF / RL)],
+                                                  const v4f (&t4)[(PAIRS * (NF / RL) + NTH - 1) / NTH]
+                                                                 [W / (NF / RL)],
                                                   int tid) {
   constexpr int NBL = NF / RL;
   constexpr int RW1 = W / NBL;
@@ -206,7 +209,7 @@ __device__ __forceinline__ void fused_select_pass(const LdsPairs& rowsF, const L
       cpx2 u[RW1];
       static_for<0, RW1>([&](auto rr) {
         constexpr int r = fused_src<NF, W, NBL, SPANS>(decltype(rr)::value);
-        u[rr] = cmul(v[p][r], t4[p][rr]);
+        u[rr] = cmul(v[p][r], from_interleaved(t4[p][rr]));
       });
       sdft<RW1, +1>(u);
       static_for<0, RW1>([&](auto rr) { rowsW.store(q, j * RW1 + rr, u[rr], p, rr); });
@@ -284,9 +287,11 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
     // Nf passes 1 .. last-1 (the first from `in`), then the fused pass, then W passes 2..
     auto run_block = [&](const auto& in, int b, auto after_first) {
       stockham_pass_pair<NF, R1, 1, -1, PAIRS, NTP>(in, rowsF, twF, tid);
-      after_first();
-      cpx2 t4[PT][RW1];
+      // the gain x twiddle loads go out BEFORE the next block's prefetch: vmcnt retires
+      // in order, so waiting for them must not mean waiting for the HBM prefetch too
+      v4f t4[PT][RW1];
       load_t4<NBL, RW1, PAIRS, NTP>(t4, tw4r, N, tid);
+      after_first();
       __syncthreads();
       if constexpr (!std::is_same_v<typename SP::Mid, Radices<>>) {
         run_fft_mid<NF, -1, PAIRS, NTP, R1>(rowsF, twF, tid, typename SP::Mid{});
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
       run_block(in, b, [] {});
     } else {
       constexpr int PF = (PAIRS * NB1 + NTP - 1) / NTP;
-      cpx2 zv[PF][R1];
+      v4f zv[PF][R1];
       static_assert(DK >= 0 && DK <= R1, "overlap reuse needs keep = DK * NF / R1");
       auto prefetch = [&](int b, auto reuse) {
         constexpr int R0 = decltype(reuse)::value ? R1 - DK : 0;  // registers kept
@@ -314,7 +319,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
           static_for<0, R0>([&](auto r) { zv[p][r] = zv[p][r + DK]; });
           static_for<R0, R1>([&](auto r) {
             const v4u x = __builtin_amdgcn_raw_buffer_load_b128(z, (j * N + 2 * q) * 8, r * NB1 * N * 8, 0);
-            zv[p][r] = from_interleaved(__builtin_bit_cast(v4f, x));
+            zv[p][r] = __builtin_bit_cast(v4f, x);
           });
         });
       };
@@ -324,7 +329,10 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
       for (int b = b_begin; b < b_end; b += b_step) {
         __syncthreads();  // tables / previous block's W transform done with the rows
         run_block(in, b, [&] {
-          if (b + b_step < b_end) prefetch(b + b_step, std::integral_constant<bool, (DK > 0)>{});
+          // unconditional (the last block re-reads itself): a conditional prefetch
+          // leaves the vmcnt count path-dependent, and the compiler then waits for the
+          // prefetch together with the gain x twiddle loads in the fused pass
+          prefetch(min(b + b_step, b_end - 1), std::integral_constant<bool, (DK > 0)>{});
         });
       }
     }
