@@ -32,8 +32,16 @@ def load(dirs):
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
-BENCH_NAME = {"analysis_fused": "analysis_fused", "analysis_stream": "analysis_fused", "fir_generic": "analysis_fir",
-              "row_fft": "synth_chan_ifft", "synth_block": "synth_block"}
+def bench_name(k):
+    """bench.py kernel class of a kernel name (pfb_profile_read classes)."""
+    if "analysis_stream" in k:
+        # the ZOUT instance (last template argument true) also runs the channel IFFT
+        return "analysis+chan_ifft" if k.rstrip(">").endswith("true") else "analysis"
+    for key, v in (("analysis_fused", "analysis"), ("fir_generic", "analysis_fir"),
+                   ("row_fft", "synth_chan_ifft"), ("synth_block", "synth_block")):
+        if key in k:
+            return v
+    return k
 
 
 def traffic_json(res):
@@ -42,7 +50,7 @@ def traffic_json(res):
     for k, cs in res.items():
         if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
             continue
-        name = next((v for key, v in BENCH_NAME.items() if key in k), k)
+        name = bench_name(k)
         rd = 2 * cs["FETCH_SIZE"] * 1024
         wr = cs["WRITE_SIZE"] * 1024
         out[name] = {"kernel": k, "read_bytes": rd, "write_bytes": wr, "bytes": rd + wr}

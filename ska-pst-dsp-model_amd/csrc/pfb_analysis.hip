@@ -203,8 +203,11 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
   uint32_t nbytes = (uint32_t)min(max(avail, (int64_t)0) * 8, (int64_t)0x7ffffff0);
   if (a.timing_mask & 1) nbytes = 0;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(xpol + row_first * N, nbytes);
+  // rows past the last window of the range (the unconditional last prefetch) re-read the
+  // last row instead: an L2 hit rather than HBM traffic nobody uses
+  const int r_last = (int)(st1 - st0 - 1) * NEW + WIN - 1;
   auto ld = [&](int r) {  // window row r (relative to row_first)
-    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (r * N + c) * 8, 0, 0);
+    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (min(r, r_last) * N + c) * 8, 0, 0);
     return __builtin_bit_cast(v2f, v);
   };
   // (re, im) as a packed pair: one v_pk_fma_f32 per complex x real tap MAC

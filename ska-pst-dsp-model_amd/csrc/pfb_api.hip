@@ -199,8 +199,9 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   const int64_t in_samples = (K_end == K_total && row0 == 0)
                                  ? n_dat
                                  : (K_end - row0) * p->M + (K_end == K_total ? n_dat - K_total * p->M : 0);
-  double bytes = (double)p->n_pol * (8.0 * in_samples + 8.0 * (K_end - row0) * p->N);
-  if (z) bytes += (double)p->n_pol * 8.0 * (K_end - std::max(row0, z_row0)) * p->N;  // + Z rows
+  // (with z: the stage-1 rows are a synthesis intermediate, not algorithmic bytes —
+  // the synthesis' algorithmic read of its input is counted by the block kernel)
+  const double bytes = (double)p->n_pol * (8.0 * in_samples + 8.0 * (K_end - row0) * p->N);
   ProfScope ps(z ? 3 : 0, bytes, s);
   HIPCHK(pfb::launch_analysis(a, s));
   return PFB_OK;
