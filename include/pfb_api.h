@@ -182,6 +182,57 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* analysis, pfb_synthesis_plan
                                  int64_t out_pol_stride, int64_t out_capacity, int64_t* n_out,
                                  void* stream);
 
+/* ---------------------------------------------------------------- data formats */
+/* Sample order of a DADA file's data section. */
+typedef enum pfb_dada_order {
+  PFB_DADA_TFP = 0,   /* time, channel, polarisation, re/im (reshape_dada_data.m:23-30,
+                         write_dada_data.m:32-50) */
+  PFB_DADA_LOWCBF = 1 /* heaps of 32 samples: [heap][chan][pol][sample], INSTRUMENT LowCBF
+                         (reshape_low_cbf_data.m:14-43, DADARead.m:74-78) */
+} pfb_dada_order;
+
+/* DADA data section (device memory, NBIT 8/16/32/64 signed integer / float samples,
+ * NDIM 1 or 2) -> [pol][t][chan] complex float32.  Replaces read_dada_file.m:36-47 +
+ * reshape_dada_data.m (and DADARead.generate, DADARead.m:58-83, incl. its cast of
+ * integer samples to floating point).  NBIT 64 is rounded to float32 (the engine's
+ * arithmetic type).  Asynchronous on `stream`. */
+pfb_status pfb_dada_unpack(const void* in, int32_t nbit, int32_t ndim, int32_t order,
+                           int64_t n_dat, int32_t n_chan, int32_t n_pol, pfb_cf32* out,
+                           int64_t out_pol_stride, void* stream);
+
+/* [pol][t][chan] complex float32 -> DADA TFP data section (NDIM 2) of NBIT 8/16/32/64;
+ * integer types follow Matlab's cast (round half away from zero, saturate).  Replaces
+ * write_dada_data.m:32-50 (data written with the class write_dada_header.m:13-22
+ * records as NBIT). */
+pfb_status pfb_dada_pack(const pfb_cf32* in, int64_t in_pol_stride, int64_t n_dat, int32_t n_chan,
+                         int32_t n_pol, void* out, int32_t nbit, void* stream);
+
+/* Channel gather: out[o][t][j] = in[o][t][src0 + j + (j >= split ? shift : 0)] for
+ * o < n_outer (<= 65535), t < n_rows, j < n_sel (strides in complex samples).
+ * Replaces the stage-2 output assembly of TwoStageFilterBank.m:102-105 (shift = the
+ * oversampled channels dropped in the middle) and the per-coarse-channel input slices
+ * of TwoStageInverseFilterBank.m:124-126.  Device memory, asynchronous. */
+pfb_status pfb_gather_channels(const pfb_cf32* in, int64_t in_outer_stride, int64_t in_row_stride,
+                               pfb_cf32* out, int64_t out_outer_stride, int64_t out_row_stride,
+                               int64_t n_outer, int64_t n_rows, int32_t n_sel, int32_t src0,
+                               int32_t split, int32_t shift, void* stream);
+
+/* Corner turn: out[o][c][r] = in[o][r][c] (r < n_rows, c < n_cols, o < n_outer).
+ * Replaces the out1(1,ich,:) channel slices TwoStageFilterBank.m:94 feeds to stage 2
+ * (channelised [t][chan] -> per-channel series).  Device memory, asynchronous. */
+pfb_status pfb_corner_turn(const pfb_cf32* in, int64_t in_outer_stride, int64_t in_row_stride,
+                           int64_t n_outer, int64_t n_rows, int64_t n_cols, pfb_cf32* out,
+                           int64_t out_outer_stride, int64_t out_row_stride, void* stream);
+
+/* Quantisation hook: out = round(single(scale) * in) with scale = rms / sqrt(var(in, 0,
+ * "all")) over all n_pol x n samples, or 1 when rms <= 0 (Matlab round: half away from
+ * zero).  Replaces FilterBank.m:75-83 (rndInput/rmsInput) and :106-113
+ * (rndOutput/rmsOutput).  in == out is allowed.  Device memory; asynchronous unless
+ * `scale` is non-null (then it receives the scale and the call synchronises). */
+pfb_status pfb_quantize(const pfb_cf32* in, int64_t in_pol_stride, int64_t n, int32_t n_pol,
+                        double rms, pfb_cf32* out, int64_t out_pol_stride, double* scale,
+                        void* stream);
+
 /* ---------------------------------------------------------------- utilities */
 const char* pfb_last_error(void);
 int32_t pfb_api_version(void);

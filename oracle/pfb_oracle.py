@@ -590,6 +590,26 @@ def calc_output_nbins(nbins, channels, os_factor, filter_taps, input_fft_length,
 
 
 # --------------------------------------------------------------------------- streaming
+def matlab_round(v: np.ndarray) -> np.ndarray:
+    """Matlab ``round``: half away from zero (numpy's ``round`` is half to even)."""
+    v = np.asarray(v, dtype=np.float64)
+    return np.trunc(v + np.copysign(0.5, v))
+
+
+def quantize(x, scale) -> np.ndarray:
+    """``complex(round(scale * x))`` on single data (FilterBank.m:82,112): the double
+    scale meets a single array, so the product is formed in single precision."""
+    y = np.float32(scale) * np.asarray(x).astype(np.complex64)
+    return (matlab_round(y.real) + 1j * matlab_round(y.imag)).astype(np.complex64)
+
+
+def quantize_scale(x, rms) -> float:
+    """rms / sqrt(var(x, 0, "all")) or 1 (FilterBank.m:76-81,107-111)."""
+    if rms > 0:
+        return float(rms / np.sqrt(np.var(np.asarray(x, dtype=np.complex128), ddof=1)))
+    return 1.0
+
+
 class FilterBankOracle:
     """FilterBank.m:26-128 — analysis with input buffering and nu-trimming."""
 
@@ -610,10 +630,8 @@ class FilterBankOracle:
         if x.ndim == 2:
             x = x[:, None, :]
         if self.rndInput:  # :75-83
-            scale = 1.0
-            if self.rmsInput > 0:
-                scale = self.rmsInput / np.sqrt(np.var(x, ddof=1))
-            x = np.round(scale * x).astype(np.complex64)
+            scale = quantize_scale(x, self.rmsInput)
+            x = quantize(x, scale)
         if self.buffered_samples > 0:  # :85-88
             x = np.concatenate([self.input_buffer, x], axis=2)
             self.buffered_samples = 0
@@ -623,10 +641,8 @@ class FilterBankOracle:
         if rem:
             out = out[:, :, :out.shape[2] - rem]
         if self.rndOutput:  # :106-113
-            scale = 1.0
-            if self.rmsOutput:
-                scale = self.rmsOutput / np.sqrt(np.var(out, ddof=1))
-            out = np.round(scale * out)
+            scale = quantize_scale(out, self.rmsOutput)
+            out = quantize(out, scale)
         input_idat = Fraction(out.shape[2] * self.n_chan * self.os_factor.de, self.os_factor.nu)
         self.buffered_samples = int(n_in - input_idat)  # :119-126
         if self.buffered_samples > 0:
@@ -764,3 +780,46 @@ class TwoStageInverseFilterBankOracle:
                 out = np.zeros((1, nch_out, tmp.shape[2]), dtype=np.complex128)
             out[0, ich, :] = tmp[0, 0, :]
         return out
+
+
+# --------------------------------------------------------------------------- DADA layout
+_NBIT_NP = {8: np.int8, 16: np.int16, 32: np.float32, 64: np.float64}
+
+
+def reshape_dada_data(data, n_dim: int, n_pol: int, n_chan: int) -> np.ndarray:
+    """reshape_dada_data.m:23-30: flat samples -> (n_pol, n_chan, n_dat), column-major
+    (Matlab ``reshape``), re/im pairs joined when n_dim == 2."""
+    d = np.asarray(data).reshape(-1).astype(np.float64)
+    if n_dim == 2:
+        d = d[0::2] + 1j * d[1::2]
+    return d.reshape((n_pol, n_chan, -1), order="F")
+
+
+def reshape_low_cbf_data(data, n_dim: int, n_pol: int, n_chan: int) -> np.ndarray:
+    """reshape_low_cbf_data.m:14-43: heaps of 32 samples, each reshaped to
+    (32, n_pol, n_chan) column-major and permuted to (n_pol, n_chan, 32)."""
+    d = np.asarray(data).reshape(-1).astype(np.float64)
+    if n_dim == 2:
+        d = d[0::2] + 1j * d[1::2]
+    per_heap = 32 * n_pol * n_chan
+    nheap = d.size // per_heap
+    out = np.zeros((n_pol, n_chan, nheap * 32), dtype=np.complex128)
+    for h in range(nheap):
+        tmp = d[h * per_heap:(h + 1) * per_heap].reshape((32, n_pol, n_chan), order="F")
+        out[:, :, h * 32:(h + 1) * 32] = np.transpose(tmp, (1, 2, 0))
+    return out
+
+
+def write_dada_data(data, nbit: int) -> np.ndarray:
+    """write_dada_data.m:32-50: (n_pol, n_chan, n_dat) complex -> flat column-major
+    samples with re/im interleaved, in the class of NBIT (Matlab cast: round half away
+    from zero and saturate for integer classes)."""
+    flat = np.asarray(data).reshape(-1, order="F")
+    inter = np.empty(2 * flat.size, dtype=np.float64)
+    inter[0::2] = flat.real
+    inter[1::2] = flat.imag
+    t = _NBIT_NP[int(nbit)]
+    if np.issubdtype(t, np.integer):
+        info = np.iinfo(t)
+        inter = np.clip(matlab_round(np.nan_to_num(inter)), info.min, info.max)
+    return inter.astype(t)

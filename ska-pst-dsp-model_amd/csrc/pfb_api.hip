@@ -141,7 +141,20 @@ struct ProfScope {
 
 int64_t floordiv(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
+// n_pol rows of n complex samples at (dst + q*dps) <- (src + q*sps): one 2-D copy, not
+// n_pol calls (the two-stage cascades run thousands of series through one plan)
+hipError_t copy_pols(float2* dst, int64_t dps, const float2* src, int64_t sps, int64_t n, int n_pol,
+                     hipMemcpyKind kind, hipStream_t s) {
+  if (n <= 0 || n_pol <= 0) return hipSuccess;
+  if (n_pol == 1) return hipMemcpyAsync(dst, src, n * sizeof(float2), kind, s);
+  return hipMemcpy2DAsync(dst, dps * sizeof(float2), src, sps * sizeof(float2), n * sizeof(float2),
+                          n_pol, kind, s);
+}
+
 }  // namespace
+
+// error channel shared with the other C-ABI translation units (pfb_layout.hip)
+pfb_status pfb_set_error(pfb_status s, const char* msg) { return fail(s, "%s", msg); }
 
 // ====================================================================== analysis plan
 struct pfb_analysis_plan {
@@ -329,15 +342,13 @@ pfb_status pfb_analysis_execute(pfb_analysis_plan* p, const pfb_cf32* in, int64_
   // host staging (synchronous)
   HIPCHK(p->stage_in.ensure((size_t)p->n_pol * n_dat * sizeof(float2)));
   HIPCHK(p->stage_out.ensure((size_t)p->n_pol * K * p->N * sizeof(float2)));
-  for (int q = 0; q < p->n_pol; ++q)
-    HIPCHK(hipMemcpyAsync(p->stage_in.as<float2>() + (size_t)q * n_dat, in + q * in_ps,
-                          n_dat * sizeof(float2), hipMemcpyHostToDevice, s));
+  HIPCHK(copy_pols(p->stage_in.as<float2>(), n_dat, (const float2*)in, in_ps, n_dat, p->n_pol,
+                   hipMemcpyHostToDevice, s));
   pfb_status st = analysis_run(p, p->stage_in.as<float2>(), n_dat, n_dat,
                                p->stage_out.as<float2>(), K * p->N, 0, K, K, s);
   if (st != PFB_OK) return st;
-  for (int q = 0; q < p->n_pol; ++q)
-    HIPCHK(hipMemcpyAsync(out + q * out_ps, p->stage_out.as<float2>() + (size_t)q * K * p->N,
-                          K * p->N * sizeof(float2), hipMemcpyDeviceToHost, s));
+  HIPCHK(copy_pols((float2*)out, out_ps, p->stage_out.as<float2>(), K * p->N, K * p->N, p->n_pol,
+                   hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   return PFB_OK;
 }
@@ -353,14 +364,9 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
   // input = cat(3, input_buffer, input)   (FilterBank.m:85-88)
   HIPCHK(p->work.ensure((size_t)p->n_pol * std::max<int64_t>(total, 1) * sizeof(float2)));
   float2* w = p->work.as<float2>();
-  for (int q = 0; q < p->n_pol; ++q) {
-    if (p->buffered > 0)
-      HIPCHK(hipMemcpyAsync(w + (size_t)q * total, p->carry.as<float2>() + (size_t)q * p->buffered,
-                            p->buffered * sizeof(float2), hipMemcpyDeviceToDevice, s));
-    if (n_in > 0)
-      HIPCHK(hipMemcpyAsync(w + (size_t)q * total + p->buffered, in + q * in_ps,
-                            n_in * sizeof(float2), kin, s));
-  }
+  HIPCHK(copy_pols(w, total, p->carry.as<float2>(), p->buffered, p->buffered, p->n_pol,
+                   hipMemcpyDeviceToDevice, s));
+  HIPCHK(copy_pols(w + p->buffered, total, (const float2*)in, in_ps, n_in, p->n_pol, kin, s));
   const int64_t K = analysis_K(p, total);
   const int64_t Kt = K - (K % p->nu);  // trim to a multiple of nu (FilterBank.m:93-104)
   if (n_out) *n_out = Kt;
@@ -386,9 +392,7 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
     if (st != PFB_OK) return st;
     if (dst != (float2*)out) {
       const hipMemcpyKind ko = mem == PFB_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
-      for (int q = 0; q < p->n_pol; ++q)
-        HIPCHK(hipMemcpyAsync(out + q * out_ps, dst + (size_t)q * dps, Kt * p->N * sizeof(float2),
-                              ko, s));
+      HIPCHK(copy_pols((float2*)out, out_ps, dst, dps, Kt * p->N, p->n_pol, ko, s));
     }
   }
   // carry = input(:,:,input_idat+1:end), input_idat = T_out N de / nu   (FilterBank.m:119-126)
@@ -397,9 +401,8 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
   if (nb > 0) {
     HIPCHK(p->carry.ensure((size_t)p->n_pol * nb * sizeof(float2)));
     // carry may alias nothing in `work` (separate buffer); copy per pol
-    for (int q = 0; q < p->n_pol; ++q)
-      HIPCHK(hipMemcpyAsync(p->carry.as<float2>() + (size_t)q * nb, w + (size_t)q * total + input_idat,
-                            nb * sizeof(float2), hipMemcpyDeviceToDevice, s));
+    HIPCHK(copy_pols(p->carry.as<float2>(), nb, w + input_idat, total, nb, p->n_pol,
+                     hipMemcpyDeviceToDevice, s));
   }
   p->buffered = std::max<int64_t>(nb, 0);
   if (mem == PFB_MEM_HOST) HIPCHK(hipStreamSynchronize(s));
@@ -771,15 +774,13 @@ pfb_status pfb_synthesis_execute(pfb_synthesis_plan* p, const pfb_cf32* in, int6
   }
   HIPCHK(p->stage_in.ensure((size_t)p->n_pol * n * p->N * sizeof(float2)));
   HIPCHK(p->stage_out.ensure((size_t)p->n_pol * olen * sizeof(float2)));
-  for (int q = 0; q < p->n_pol; ++q)
-    HIPCHK(hipMemcpyAsync(p->stage_in.as<float2>() + (size_t)q * n * p->N, in + q * in_ps + off * p->N,
-                          n * p->N * sizeof(float2), hipMemcpyHostToDevice, s));
+  HIPCHK(copy_pols(p->stage_in.as<float2>(), n * p->N, (const float2*)in + off * p->N, in_ps,
+                   n * p->N, p->n_pol, hipMemcpyHostToDevice, s));
   pfb_status st = synthesis_run(p, p->stage_in.as<float2>(), n * p->N, n, p->stage_out.as<float2>(),
                                 olen, olen, s);
   if (st != PFB_OK) return st;
-  for (int q = 0; q < p->n_pol; ++q)
-    HIPCHK(hipMemcpyAsync(out + q * out_ps, p->stage_out.as<float2>() + (size_t)q * olen,
-                          olen * sizeof(float2), hipMemcpyDeviceToHost, s));
+  HIPCHK(copy_pols((float2*)out, out_ps, p->stage_out.as<float2>(), olen, olen, p->n_pol,
+                   hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   return PFB_OK;
 }
@@ -795,14 +796,10 @@ pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* p, const pfb_cf32*
   const hipMemcpyKind kin = mem == PFB_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
   HIPCHK(p->work.ensure((size_t)p->n_pol * std::max<int64_t>(total, 1) * N * sizeof(float2)));
   float2* w = p->work.as<float2>();
-  for (int q = 0; q < p->n_pol; ++q) {
-    if (p->buffered > 0)
-      HIPCHK(hipMemcpyAsync(w + (size_t)q * total * N, p->carry.as<float2>() + (size_t)q * p->buffered * N,
-                            p->buffered * N * sizeof(float2), hipMemcpyDeviceToDevice, s));
-    if (n_in > 0)
-      HIPCHK(hipMemcpyAsync(w + (size_t)q * total * N + p->buffered * N, in + q * in_ps,
-                            n_in * N * sizeof(float2), kin, s));
-  }
+  HIPCHK(copy_pols(w, total * N, p->carry.as<float2>(), p->buffered * N, p->buffered * N, p->n_pol,
+                   hipMemcpyDeviceToDevice, s));
+  HIPCHK(copy_pols(w + p->buffered * N, total * N, (const float2*)in, in_ps, n_in * N, p->n_pol, kin,
+                   s));
   // output length and carry-over rounded up to a multiple of nu (InverseFilterBank.m:104-135)
   const int64_t B = synth_blocks(p, total);
   const int64_t full = B * p->Lkeep;
@@ -825,9 +822,8 @@ pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* p, const pfb_cf32*
       HIPCHK(p->stage_out.ensure((size_t)p->n_pol * olen * sizeof(float2)));
       pfb_status st = synthesis_run(p, w, total * N, total, p->stage_out.as<float2>(), olen, olen, s);
       if (st != PFB_OK) return st;
-      for (int q = 0; q < p->n_pol; ++q)
-        HIPCHK(hipMemcpyAsync(out + q * out_ps, p->stage_out.as<float2>() + (size_t)q * olen,
-                              olen * sizeof(float2), hipMemcpyDeviceToHost, s));
+      HIPCHK(copy_pols((float2*)out, out_ps, p->stage_out.as<float2>(), olen, olen, p->n_pol,
+                       hipMemcpyDeviceToHost, s));
     } else {
       pfb_status st = synthesis_run(p, w, total * N, total, (float2*)out, out_ps, olen, s);
       if (st != PFB_OK) return st;
@@ -835,10 +831,8 @@ pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* p, const pfb_cf32*
   }
   if (buffered > 0) {
     HIPCHK(p->carry.ensure((size_t)p->n_pol * buffered * N * sizeof(float2)));
-    for (int q = 0; q < p->n_pol; ++q)
-      HIPCHK(hipMemcpyAsync(p->carry.as<float2>() + (size_t)q * buffered * N,
-                            w + (size_t)q * total * N + input_idat * N, buffered * N * sizeof(float2),
-                            hipMemcpyDeviceToDevice, s));
+    HIPCHK(copy_pols(p->carry.as<float2>(), buffered * N, w + input_idat * N, total * N, buffered * N,
+                     p->n_pol, hipMemcpyDeviceToDevice, s));
   }
   p->buffered = std::max<int64_t>(buffered, 0);
   if (mem == PFB_MEM_HOST) HIPCHK(hipStreamSynchronize(s));

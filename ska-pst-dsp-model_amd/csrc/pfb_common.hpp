@@ -161,7 +161,10 @@ __global__ __launch_bounds__(NT) void row_fft_kernel(RowFftArgs a) {
   constexpr int TPT = (N + NT - 1) / NT;
   float2 twv[TPT];
 #pragma unroll
-  for (int i = 0; i < TPT; ++i) twv[i] = a.tw[(threadIdx.x + i * NT) & (N - 1)];
+  for (int i = 0; i < TPT; ++i) {
+    const int m = threadIdx.x + i * NT;
+    twv[i] = a.tw[m < N ? m : 0];
+  }
 #pragma unroll
   for (int i = 0; i < TPT; ++i)
     if (threadIdx.x + i * NT < N) tw[threadIdx.x + i * NT] = twv[i];
@@ -190,6 +193,14 @@ inline int cu_count() {
   return n;
 }
 
+
+// non-power-of-two channel counts of the synthesis stage-1 IFFT: the critically
+// sampled / combined inputs of the two-stage inversion (nch2 = N de/nu, times combine;
+// TwoStageInverseFilterBank.m:102-118)
+inline bool mixed_chan_supported(int N) {
+  return N == 14 || N == 28 || N == 56 || N == 112 || N == 216 || N == 224 || N == 432 ||
+         N == 448 || N == 864;
+}
 
 inline bool pow2_supported(int N) {
   return N == 8 || N == 16 || N == 32 || N == 64 || N == 128 || N == 256 || N == 512 ||

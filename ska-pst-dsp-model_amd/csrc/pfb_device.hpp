@@ -234,6 +234,12 @@ template <> struct FFTPlan<216> { using type = Radices<8, 27>; };
 template <> struct FFTPlan<224> { using type = Radices<16, 14>; };
 template <> struct FFTPlan<448> { using type = Radices<16, 28>; };
 template <> struct FFTPlan<896> { using type = Radices<16, 8, 7>; };
+// critically sampled channel counts (two-stage inversion, see mixed_chan_supported)
+template <> struct FFTPlan<14> { using type = Radices<14>; };
+template <> struct FFTPlan<28> { using type = Radices<4, 7>; };
+template <> struct FFTPlan<56> { using type = Radices<8, 7>; };
+template <> struct FFTPlan<432> { using type = Radices<16, 27>; };
+template <> struct FFTPlan<864> { using type = Radices<16, 6, 9>; };
 
 // Default LDS accessors for a batch of rows stored at base + row * rs.
 struct LdsIO {

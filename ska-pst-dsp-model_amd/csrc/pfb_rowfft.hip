@@ -40,14 +40,29 @@ hipError_t dispatch_row_fft(int N, const RowFftArgs& r, int n_pol, hipStream_t s
     case 1024: return launch_row_fft<1024, DIR>(r, n_pol, s);
     case 2048: return launch_row_fft<2048, DIR>(r, n_pol, s);
     case 4096: return launch_row_fft<4096, DIR>(r, n_pol, s);
-    default: return hipErrorInvalidValue;
+    default: break;
   }
+  if constexpr (DIR > 0) {
+    switch (N) {
+      case 14: return launch_row_fft<14, DIR>(r, n_pol, s);
+      case 28: return launch_row_fft<28, DIR>(r, n_pol, s);
+      case 56: return launch_row_fft<56, DIR>(r, n_pol, s);
+      case 112: return launch_row_fft<112, DIR>(r, n_pol, s);
+      case 216: return launch_row_fft<216, DIR>(r, n_pol, s);
+      case 224: return launch_row_fft<224, DIR>(r, n_pol, s);
+      case 432: return launch_row_fft<432, DIR>(r, n_pol, s);
+      case 448: return launch_row_fft<448, DIR>(r, n_pol, s);
+      case 864: return launch_row_fft<864, DIR>(r, n_pol, s);
+      default: break;
+    }
+  }
+  return hipErrorInvalidValue;
 }
 
 template hipError_t dispatch_row_fft<-1>(int, const RowFftArgs&, int, hipStream_t);
 template hipError_t dispatch_row_fft<+1>(int, const RowFftArgs&, int, hipStream_t);
 
-bool chan_ifft_supported(int N) { return pow2_supported(N); }
+bool chan_ifft_supported(int N) { return pow2_supported(N) || mixed_chan_supported(N); }
 
 hipError_t launch_chan_ifft(const ChanIfftArgs& c, hipStream_t s) {
   if (c.n_rows <= 0) return hipSuccess;

@@ -16,7 +16,7 @@ from .filterbank import (Channelizer, DeChannelizer, FilterBank, InverseFilterBa
 from .firio import (design_PFB_FIR_filter, design_PFB_FIR_filter_two_stage,
                     read_fir_filter_coeff)
 from .window import PFBWindow, identity_taper
-from . import sharding
+from . import dada, harness, layout, sharding
 
 __all__ = [
     "PfbError", "device_count", "Rational", "default_config", "load_config", "AnalysisPlan",

@@ -35,6 +35,9 @@ PFB_WINDOW_TOP_HAT = 2
 PFB_WINDOW_HANN = 3
 PFB_WINDOW_CUSTOM = 4
 
+PFB_DADA_TFP = 0
+PFB_DADA_LOWCBF = 1
+
 _STATUS_NAMES = {
     0: "PFB_OK", 1: "PFB_ERR_INVALID_ARG", 2: "PFB_ERR_UNSUPPORTED", 3: "PFB_ERR_HIP",
     4: "PFB_ERR_OOM", 5: "PFB_ERR_BUFFER_TOO_SMALL", 6: "PFB_ERR_NO_DEVICE",
@@ -90,6 +93,17 @@ SYMBOLS = [
     ("pfb_roundtrip_execute", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                         c_void_p, c_int64, c_int64, POINTER(c_int64), c_int64,
                                         c_void_p, c_int64, c_int64, POINTER(c_int64), c_void_p]),
+    ("pfb_dada_unpack", c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int64, c_int32,
+                                  c_int32, c_void_p, c_int64, c_void_p]),
+    ("pfb_dada_pack", c_int32, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int32,
+                                c_void_p]),
+    ("pfb_gather_channels", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
+                                      c_int64, c_int64, c_int32, c_int32, c_int32, c_int32,
+                                      c_void_p]),
+    ("pfb_corner_turn", c_int32, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
+                                  c_void_p, c_int64, c_int64, c_void_p]),
+    ("pfb_quantize", c_int32, [c_void_p, c_int64, c_int64, c_int32, c_double, c_void_p, c_int64,
+                               POINTER(c_double), c_void_p]),
     ("pfb_last_error", c_char_p, []),
     ("pfb_api_version", c_int32, []),
     ("pfb_device_count", c_int32, []),

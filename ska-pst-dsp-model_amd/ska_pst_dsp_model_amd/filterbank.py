@@ -13,7 +13,7 @@ from types import SimpleNamespace
 
 import numpy as np
 
-from . import _lib
+from . import _lib, layout
 from .config import as_rational
 from .core import AnalysisPlan, SynthesisPlan, is_device_array
 from .firio import read_fir_filter_coeff
@@ -56,20 +56,24 @@ def _npol(x):
     return 1 if len(tuple(x.shape)) == 1 else int(tuple(x.shape)[0])
 
 
-def _quantize(x, rms):
-    """round(scale * x) with scale = rms / std(x) (FilterBank.m:75-83,106-113)."""
+def _to_device(x, device):
+    """(array, was_host): host arrays go to the plan's device (torch as allocator)."""
     if is_device_array(x):
-        import torch
-        scale = 1.0
-        if rms > 0:
-            scale = rms / torch.sqrt(torch.var(x.reshape(-1).to(torch.complex128))).item()
-        y = x * scale
-        return torch.complex(torch.round(y.real), torch.round(y.imag)).to(torch.complex64)
-    x = np.asarray(x)
-    scale = 1.0
-    if rms > 0:
-        scale = rms / np.sqrt(np.var(x, ddof=1))
-    return np.round(scale * x).astype(np.complex64)
+        return x, False
+    import torch
+    arr = np.ascontiguousarray(np.asarray(x), dtype=np.complex64)
+    return torch.from_numpy(arr).to(torch.device("cuda", int(device))), True
+
+
+def _to_host(x):
+    return x.cpu().numpy()
+
+
+def _quantize(x, rms, device=0):
+    """round(rms / std(x) * x) (FilterBank.m:75-83,106-113) through pfb_quantize."""
+    xd, host = _to_device(x, device)
+    y = layout.quantize(xd, rms)
+    return _to_host(y) if host else y
 
 
 class FilterBank(Channelizer):
@@ -112,11 +116,11 @@ class FilterBank(Channelizer):
     def execute(self, input):  # noqa: A002
         x = input
         if self.rndInput:
-            x = _quantize(x, self.rmsInput)
+            x = _quantize(x, self.rmsInput, self.device)
         plan = self._ensure_plan(_npol(x))
         out = plan.execute(x, stateful=True)  # (n_pol, T_out, n_chan)
         if self.rndOutput:
-            out = _quantize(out, self.rmsOutput)
+            out = _quantize(out, self.rmsOutput, self.device)
         view = out.transpose(1, 2) if is_device_array(out) else out.transpose(0, 2, 1)
         return self, view
 
@@ -200,7 +204,14 @@ class InverseFilterBank(DeChannelizer):
 
 
 class TwoStageFilterBank(Channelizer):
-    """TwoStageFilterBank.m:1-118 — stage 2 cascaded over every stage-1 channel (pol 1)."""
+    """TwoStageFilterBank.m:1-118 — stage 2 cascaded over every stage-1 channel (pol 1).
+
+    The Matlab object runs nch1 independent FilterBank objects in a loop (:92-110).
+    Here stage 2 is ONE batched plan whose "polarisations" are the nch1 stage-1
+    channels (each keeps its own carry-over, as the separate objects do): a corner
+    turn (``pfb_corner_turn``) makes the per-channel series, one analysis launch
+    channelises all of them, and one gather (``pfb_gather_channels``) assembles the
+    output with the oversampled channels chomped out (:102-105)."""
 
     def __init__(self, config, device: int = 0):
         self.stage1 = FilterBank(config, device=device)
@@ -211,7 +222,7 @@ class TwoStageFilterBank(Channelizer):
         self.critical = 0
         self.single = 0
         self.built = False
-        self.stage2 = []
+        self.stage2 = None
         self.device = device
 
     def set_stage2_config(self, config):
@@ -220,43 +231,46 @@ class TwoStageFilterBank(Channelizer):
         return self
 
     def build(self):
-        self.stage2 = [FilterBank(self.config2, device=self.device)
-                       for _ in range(self.stage1.n_chan)]
+        self.stage2 = FilterBank(self.config2, device=self.device)
         self.built = True
         return self
 
     def execute(self, input):  # noqa: A002
-        _, out1 = self.stage1.execute(input)
+        x, host = _to_device(input, self.device)
+        _, out1 = self.stage1.execute(x)          # (n_pol, nch1, T1) view
         if not self.built:
             self.build()
         os_ = self.stage1.os_factor
         nch1 = self.stage1.n_chan
-        nch2_orig = self.stage2[0].n_chan
+        nch2_orig = self.stage2.n_chan
         nch2 = (nch2_orig * os_.de) // os_.nu if self.critical else nch2_orig
         offset = nch2_orig - nch2
         if self.single == 1:
             nch1 = 1
-        out = None
-        dev = is_device_array(out1)
-        for ich in range(nch1):
-            _, tmp = self.stage2[ich].execute(out1[0:1, ich, :])
-            if out is None:
-                if dev:
-                    import torch
-                    out = torch.zeros((1, nch1 * nch2, tmp.shape[2]), dtype=torch.complex64,
-                                      device=out1.device)
-                else:
-                    out = np.zeros((1, nch1 * nch2, tmp.shape[2]), dtype=np.complex64)
-            base = ich * nch2
-            # TwoStageFilterBank.m:104-105 (index nch2/2 written twice)
-            out[0, base:base + nch2 // 2, :] = tmp[0, :nch2 // 2, :]
-            out[0, base + nch2 // 2 - 1:base + nch2, :] = \
-                tmp[0, nch2 // 2 - 1 + offset:nch2 + offset, :]
-        return self, out
+        # per-channel series of pol 1: (T1, nch1) rows -> (nch1, T1)
+        rows = out1[0].transpose(0, 1)[:, :nch1]  # (T1, nch1) view of the engine buffer
+        series = layout.corner_turn(rows)         # (nch1, T1)
+        _, tmp = self.stage2.execute(series)      # (nch1, nch2_orig, T2) view
+        buf2 = tmp.transpose(1, 2)                # (nch1, T2, nch2_orig) engine buffer
+        T2 = int(buf2.shape[1])
+        import torch
+        out = torch.empty((1, T2, nch1 * nch2), dtype=torch.complex64, device=buf2.device)
+        # out[t][ich*nch2 + j] = tmp[ich][t][j (+ offset from j = nch2/2 - 1 on)]
+        layout.gather_channels(buf2, n_outer=nch1, in_outer_stride=buf2.stride(0),
+                               in_row_stride=buf2.stride(1), n_rows=T2, n_sel=nch2,
+                               split=nch2 // 2 - 1, shift=offset, out=out,
+                               out_outer_stride=nch2, out_row_stride=nch1 * nch2)
+        view = out.transpose(1, 2)                # (1, nch1*nch2, T2)
+        return self, (_to_host(view) if host else view)
 
 
 class TwoStageInverseFilterBank(DeChannelizer):
-    """TwoStageInverseFilterBank.m:1-159 — stage-2 inversion per output coarse channel."""
+    """TwoStageInverseFilterBank.m:1-159 — stage-2 inversion per output coarse channel.
+
+    The nch_out InverseFilterBank objects of the Matlab loop (:124-151) become ONE
+    batched synthesis plan over nch_out "polarisations": one gather
+    (``pfb_gather_channels``) slices the nch_in = nch2 * combine fine channels of every
+    coarse channel, one synthesis call inverts them all."""
 
     def __init__(self, config, device: int = 0):
         self.config1 = config
@@ -267,7 +281,8 @@ class TwoStageInverseFilterBank(DeChannelizer):
         self.single = 0
         self.combine = 1
         self.built = False
-        self.stage2 = []
+        self.stage2 = None
+        self._ftaper = None
         self.device = device
 
     def set_stage2_config(self, config):
@@ -276,25 +291,29 @@ class TwoStageInverseFilterBank(DeChannelizer):
         return self
 
     def build(self):
-        self.stage2 = [InverseFilterBank(self.config2, device=self.device)
-                       for _ in range(self.nch1)]
+        self.stage2 = InverseFilterBank(self.config2, device=self.device)
+        if self._ftaper is not None:
+            self.stage2.frequency_taper(self._ftaper)
         self.built = True
         return self
 
     def frequency_taper(self, name):
+        self._ftaper = name
         if not self.built:
             self.build()
-        for st in self.stage2:
-            st.frequency_taper(name)
+        self.stage2.frequency_taper(name)
         return self
 
     def execute(self, input):  # noqa: A002
         if not self.built:
             self.build()
+        x, host = _to_device(input, self.device)
+        if not x.is_complex():
+            raise ValueError("input data are real !")
         os_ = self.stage1.os_factor
-        npol, nchan = int(input.shape[0]), int(input.shape[1])
+        npol, nchan, T = (int(v) for v in x.shape)
         nch_out = nchan // self.nch2
-        stage2_nchan = self.stage2[0].nchan
+        stage2_nchan = self.stage2.nchan
         critical_stage2_nchan = (stage2_nchan * os_.de) // os_.nu
         if self.nch2 == critical_stage2_nchan:
             critical = True
@@ -309,19 +328,14 @@ class TwoStageInverseFilterBank(DeChannelizer):
         nch_out = nch_out // self.combine
         if self.single:
             nch_out = 1
-        out = None
-        dev = is_device_array(input)
-        for ich in range(nch_out):
-            st = self.stage2[ich]
-            st.critical = critical
-            st.combine = self.combine
-            _, tmp = st.execute(input[0:1, ich * nch_in:(ich + 1) * nch_in, :])
-            if out is None:
-                if dev:
-                    import torch
-                    out = torch.zeros((1, nch_out, tmp.shape[2]), dtype=torch.complex64,
-                                      device=input.device)
-                else:
-                    out = np.zeros((1, nch_out, tmp.shape[2]), dtype=np.complex64)
-            out[0, ich, :] = tmp[0, 0, :]
-        return self, out
+        buf = x.transpose(1, 2)                   # (npol, T, nchan) engine order
+        if buf.stride(2) != 1:
+            buf = buf.contiguous()
+        sliced = layout.gather_channels(buf[0], n_outer=nch_out, in_outer_stride=nch_in,
+                                        in_row_stride=buf.stride(1), n_rows=T, n_sel=nch_in)
+        st = self.stage2
+        st.critical = critical
+        st.combine = self.combine
+        _, tmp = st.execute(sliced.transpose(1, 2))  # (nch_out, 1, T_out)
+        out = tmp.reshape(1, nch_out, tmp.shape[2])
+        return self, (_to_host(out) if host else out)

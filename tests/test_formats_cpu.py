@@ -1,0 +1,91 @@
+"""CPU tests of the data-format host logic: DADA header read/write (read_header.m,
+write_header.m semantics), the oracle's layout restatements and Matlab rounding,
+and the harness' naming helpers.  No device needed."""
+import io
+
+import numpy as np
+
+from oracle import pfb_oracle as orc
+
+
+def _dada():
+    from ska_pst_dsp_model_amd import dada
+    return dada
+
+
+def test_header_round_trip_and_order():
+    dada = _dada()
+    hdr = {"NCHAN": "256", "HDR_SIZE": "4096", "OS_FACTOR": "8/7", "A_KEY": "1"}
+    f = io.BytesIO()
+    dada.write_header(f, hdr)
+    raw = f.getvalue()
+    assert len(raw) == 4096
+    text = raw.rstrip(b"\0").decode()
+    lines = text.strip("\n").split("\n")
+    assert lines[0] == "HDR_SIZE 4096"
+    assert lines[1:] == ["A_KEY 1", "NCHAN 256", "OS_FACTOR 8/7"]  # containers.Map order
+    assert dada.read_header(io.BytesIO(raw)) == hdr
+
+
+def test_header_grows_when_too_long():
+    dada = _dada()
+    hdr = {"HDR_SIZE": "4096", "COEFF_0": ",".join(["1.000000E+00"] * 500)}
+    f = io.BytesIO()
+    dada.write_header(f, hdr)
+    raw = f.getvalue()
+    assert len(raw) == 8192
+    h = dada.read_header(io.BytesIO(raw + b"\x01" * 100))
+    assert h["HDR_SIZE"] == "8192" and h["COEFF_0"] == hdr["COEFF_0"]
+
+
+def test_header_comments_and_missing_size():
+    dada = _dada()
+    text = b"# comment line\nHDR_VERSION 1.0\nNBIT 8 trailing words\n"
+    h = dada.read_header(io.BytesIO(text))
+    assert h == {"HDR_VERSION": "1.0", "NBIT": "8"}
+
+
+def test_add_fir_filter_to_header():
+    dada = _dada()
+    h = dada.add_fir_filter_to_header({}, np.array([0.5, -1.25e-3]), "8/7")
+    assert h == {"NSTAGE": "1", "COEFF_0": "5.000000E-01,-1.250000E-03", "OVERSAMP_0": "8/7",
+                 "NTAP_0": "2"}
+
+
+def test_matlab_round_half_away_from_zero():
+    v = np.array([0.5, -0.5, 1.5, -1.5, 2.5, -2.5, 0.49999997, 2.0])
+    assert np.array_equal(orc.matlab_round(v), [1, -1, 2, -2, 3, -3, 0, 2])
+
+
+def test_oracle_dada_layouts():
+    # TFP: sample index = p + P (c + C t), re/im interleaved
+    P, C, T = 2, 3, 5
+    x = np.arange(P * C * T) * (1 + 2j)
+    x = x.reshape((P, C, T), order="F")
+    flat = orc.write_dada_data(x, 64)
+    for p in range(P):
+        for c in range(C):
+            for t in range(T):
+                e = p + P * (c + C * t)
+                assert flat[2 * e] == x[p, c, t].real and flat[2 * e + 1] == x[p, c, t].imag
+    assert np.array_equal(orc.reshape_dada_data(flat, 2, P, C), x)
+    # LowCBF heap: [heap][chan][pol][sample]
+    raw = np.arange(2 * P * C * 32 * 2, dtype=np.float64)
+    y = orc.reshape_low_cbf_data(raw, 2, P, C)
+    h, c, p, s = 1, 2, 1, 7
+    e = ((h * C + c) * P + p) * 32 + s
+    assert y[p, c, h * 32 + s] == raw[2 * e] + 1j * raw[2 * e + 1]
+
+
+def test_oracle_write_saturates_integers():
+    x = np.array([[[300.4 - 300.6j, 127.5 + 0.5j, -128.5 - 0.49j]]])
+    assert orc.write_dada_data(x, 8).tolist() == [127, -128, 127, 1, -128, 0]
+
+
+def test_harness_names():
+    from ska_pst_dsp_model_amd import harness
+    assert harness.create_output_file_names(None, "a.b") == ("a.b", "a.b.log", "a.b.dump")
+    assert harness.create_output_file_names("x.dump", "q") == ("x", "x.log", "x.dump")
+    assert harness._num2str(241.92) == "241.92"
+    assert harness._num2str(2.0) == "2"
+    assert harness._num2str(1.0 / 7) == "0.14286"

@@ -1,0 +1,248 @@
+"""GPU parity of the data-format kernels (pfb_layout.hip) and of the stream objects
+built on them: DADA unpack/pack, corner turn, channel gather, quantisation hooks,
+the batched two-stage cascades and the ``hip`` harness backend.
+
+Integer/byte work is checked bit-exactly; the filter-bank stages keep the reference's
+1e-6 (conftest.assert_pfb_close).
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_pfb_close
+from oracle import pfb_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _pfb():
+    import ska_pst_dsp_model_amd as pfb
+    return pfb
+
+
+def _noise(rng, shape, scale=1.0):
+    return (scale * (rng.standard_normal(shape) + 1j * rng.standard_normal(shape)) /
+            np.sqrt(2)).astype(np.complex64)
+
+
+def _file_samples(rng, nbit, count):
+    t = orc._NBIT_NP[nbit]
+    if np.issubdtype(t, np.integer):
+        info = np.iinfo(t)
+        return rng.integers(info.min, info.max + 1, size=count).astype(t)
+    return rng.standard_normal(count).astype(t)
+
+
+# ----------------------------------------------------------------------------- DADA
+@pytest.mark.parametrize("nbit", [8, 16, 32, 64])
+@pytest.mark.parametrize("ndim,n_pol,n_chan", [(2, 1, 1), (2, 2, 1), (2, 2, 256), (1, 2, 8),
+                                               (2, 1, 7)])
+def test_dada_unpack_matches_reshape(gpu, nbit, ndim, n_pol, n_chan):
+    import torch
+    from ska_pst_dsp_model_amd import layout
+    rng = np.random.default_rng(nbit * 100 + n_chan)
+    n_dat = 1000
+    raw = _file_samples(rng, nbit, n_dat * n_chan * n_pol * ndim)
+    got = layout.dada_unpack(torch.from_numpy(raw.view(np.uint8)).to(gpu), nbit, ndim, n_chan,
+                             n_pol)
+    ref = orc.reshape_dada_data(raw, ndim, n_pol, n_chan)          # (n_pol, n_chan, n_dat)
+    ref = ref.transpose(0, 2, 1).astype(np.complex64)               # engine (pol, t, chan)
+    assert np.array_equal(got.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("nbit", [8, 16])
+def test_dada_unpack_lowcbf_heaps(gpu, nbit):
+    import torch
+    from ska_pst_dsp_model_amd import layout
+    rng = np.random.default_rng(7)
+    n_pol, n_chan, n_dat = 2, 6, 32 * 5
+    raw = _file_samples(rng, nbit, n_dat * n_chan * n_pol * 2)
+    got = layout.dada_unpack(torch.from_numpy(raw.view(np.uint8)).to(gpu), nbit, 2, n_chan,
+                             n_pol, lowcbf=True)
+    ref = orc.reshape_low_cbf_data(raw, 2, n_pol, n_chan).transpose(0, 2, 1)
+    assert np.array_equal(got.cpu().numpy(), ref.astype(np.complex64))
+
+
+@pytest.mark.parametrize("nbit", [8, 16, 32, 64])
+def test_dada_pack_matches_write_dada_data(gpu, nbit):
+    import torch
+    from ska_pst_dsp_model_amd import layout
+    rng = np.random.default_rng(nbit)
+    x = _noise(rng, (2, 333, 16), scale=300.0)                      # engine (pol, t, chan)
+    x[0, 0, :4] = [0.5, -0.5, 1.5 - 2.5j, 1e6]                      # ties and saturation
+    got = layout.dada_pack(torch.from_numpy(x).to(gpu), nbit).cpu().numpy()
+    ref = orc.write_dada_data(x.transpose(0, 2, 1), nbit)           # Matlab (pol, chan, t)
+    assert np.array_equal(got, ref)
+
+
+def test_dada_file_round_trip(gpu, tmp_path):
+    pfb = _pfb()
+    rng = np.random.default_rng(3)
+    x = _noise(rng, (2, 4, 500))                                    # Matlab (pol, chan, t)
+    hdr = {"HDR_SIZE": "4096", "TSAMP": "1.08", "INSTRUMENT": "dspsr", "SOURCE": "x y"}
+    p = tmp_path / "a.dada"
+    h = pfb.dada.write_dada_file(p, x, hdr)
+    assert h["NPOL"] == "2" and h["NCHAN"] == "4" and h["NBIT"] == "32" and h["NDIM"] == "2"
+    raw = p.read_bytes()
+    assert len(raw) == 4096 + x.size * 8
+    assert np.array_equal(np.frombuffer(raw[4096:], dtype=np.float32), orc.write_dada_data(x, 32))
+    d, h2 = pfb.dada.read_dada_file(p)
+    assert np.array_equal(d.cpu().numpy(), x)
+    assert h2["SOURCE"] == "x"  # first token only (read_header.m strsplit)
+    r = pfb.dada.DADARead().open(p)
+    _, a = r.generate(200)
+    _, b = r.generate(300)
+    r.close()
+    assert np.array_equal(np.concatenate([a.cpu().numpy(), b.cpu().numpy()], axis=2), x)
+
+
+# ----------------------------------------------------------------------------- layout
+def test_corner_turn_and_gather(gpu):
+    import torch
+    from ska_pst_dsp_model_amd import layout
+    rng = np.random.default_rng(5)
+    x = _noise(rng, (3, 1037, 45))
+    xd = torch.from_numpy(x).to(gpu)
+    assert np.array_equal(layout.corner_turn(xd).cpu().numpy(), x.transpose(0, 2, 1))
+    assert np.array_equal(layout.corner_turn(xd[1]).cpu().numpy(), x[1].T)
+    flat = x[0]                                                     # (1037 rows, 45 chans)
+    g = layout.gather_channels(xd[0], n_outer=5, in_outer_stride=9, in_row_stride=45,
+                               n_rows=1037, n_sel=9).cpu().numpy()
+    assert np.array_equal(g, flat.reshape(1037, 5, 9).transpose(1, 0, 2))
+    # two-stage chomp: j < split -> j, else j + shift
+    g2 = layout.gather_channels(xd[0], n_outer=1, in_outer_stride=0, in_row_stride=45,
+                                n_rows=1037, n_sel=8, src0=2, split=3, shift=4).cpu().numpy()
+    idx = [2 + j + (4 if j >= 3 else 0) for j in range(8)]
+    assert np.array_equal(g2[0], flat[:, idx])
+
+
+def test_gather_rejects_out_of_row(gpu):
+    import torch
+    pfb = _pfb()
+    from ska_pst_dsp_model_amd import layout
+    x = torch.zeros((10, 8), dtype=torch.complex64, device=gpu)
+    with pytest.raises(pfb.PfbError):
+        layout.gather_channels(x, n_outer=1, in_outer_stride=0, in_row_stride=8, n_rows=10,
+                               n_sel=8, shift=1, split=4)
+
+
+# ----------------------------------------------------------------------------- quantisation
+def test_quantize_round_half_away(gpu):
+    import torch
+    from ska_pst_dsp_model_amd import layout
+    v = np.array([0.5, -0.5, 1.5, -1.5, 2.5, 0.49999997, -2.4999998, 3.0], dtype=np.float32)
+    x = (v + 1j * v[::-1]).astype(np.complex64)[None, :]
+    got = layout.quantize(torch.from_numpy(x).to(gpu), 0.0).cpu().numpy()
+    assert np.array_equal(got, orc.quantize(x, 1.0))
+    assert np.array_equal(got.real[0], [1, -1, 2, -2, 3, 0, -2, 3])
+
+
+def test_quantize_rms_scale(gpu):
+    import torch
+    from ska_pst_dsp_model_amd import layout
+    rng = np.random.default_rng(11)
+    x = _noise(rng, (2, 1 << 16), scale=3.0) + np.complex64(0.25 - 0.5j)
+    got, sc = layout.quantize(torch.from_numpy(x).to(gpu), 33.8, return_scale=True)
+    ref_sc = orc.quantize_scale(x, 33.8)
+    assert abs(sc - ref_sc) <= 1e-9 * ref_sc
+    ref = orc.quantize(x, ref_sc)
+    d = np.abs(got.cpu().numpy() - ref)
+    # the device scale agrees to ~1e-12; a product landing within an ulp of a .5 tie may
+    # round the other way (at most 1 unit), which must be vanishingly rare
+    assert d.max() <= 1.0 and (d > 0).mean() < 1e-4
+
+
+def test_filterbank_quantisation_hooks(gpu):
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(8, "8/7", 10)
+    cfg = dict(analysis_function="polyphase_analysis", filt_coeff=taps, channels=8,
+               os_factor="8/7", rndInput=True, rmsInput=0.0, rndOutput=True, rmsOutput=0.0)
+    fb = pfb.FilterBank(cfg)
+    ofb = orc.FilterBankOracle(taps, 8, "8/7", rndInput=True, rndOutput=True)
+    rng = np.random.default_rng(12)
+    for n in (1500, 900, 2100):
+        x = _noise(rng, (2, 1, n), scale=20.0)
+        fb, got = fb.execute(x)
+        ref = ofb.execute(x)
+        assert got.shape == ref.shape
+        # analysis outputs agree to 1e-6 of the peak; rounding them can flip a value
+        # sitting on a .5 boundary, so compare integers with a 1-unit allowance
+        d = np.abs(np.asarray(got) - ref)
+        assert d.max() <= 1.0 and (d > 0).mean() < 1e-3
+        assert fb.buffered_samples == ofb.buffered_samples
+
+
+# ----------------------------------------------------------------------------- two stage
+def _fb_cfg(taps, N, os_="8/7"):
+    return dict(analysis_function="polyphase_analysis", filt_coeff=taps, channels=N,
+                os_factor=os_)
+
+
+@pytest.mark.parametrize("critical,single", [(0, 0), (1, 0), (0, 1)])
+def test_two_stage_filterbank_matches_oracle(gpu, critical, single):
+    pfb = _pfb()
+    taps1 = pfb.design_PFB_FIR_filter(8, "8/7", 10)
+    taps2 = pfb.design_PFB_FIR_filter(16, "8/7", 10)
+    ts = pfb.TwoStageFilterBank(_fb_cfg(taps1, 8)).set_stage2_config(_fb_cfg(taps2, 16))
+    ts.critical, ts.single = critical, single
+    ots = orc.TwoStageFilterBankOracle(orc.FilterBankOracle(taps1, 8, "8/7"),
+                                       lambda: orc.FilterBankOracle(taps2, 16, "8/7"),
+                                       critical=bool(critical), single=bool(single))
+    rng = np.random.default_rng(21)
+    for n in (40000, 23456):  # two calls: per-channel carry-over in the batched plan
+        x = _noise(rng, (2, 1, n))
+        ts, got = ts.execute(x)
+        ref = ots.execute(x)
+        assert_pfb_close(got, ref, what=f"two-stage n={n}")
+
+
+@pytest.mark.parametrize("critical,combine", [(False, 1), (True, 1), (True, 2)])
+def test_two_stage_inverse_matches_oracle(gpu, critical, combine):
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(16, "8/7", 10)
+    cfg = dict(filt_coeff=taps, channels=16, os_factor="8/7", input_fft_length=128,
+               input_overlap=16, deripple=False, temporal_taper="tukey")
+    nch2 = 14 if critical else 16
+    n_coarse = 4
+    ti = pfb.TwoStageInverseFilterBank(cfg)
+    ti.nch2 = nch2
+    ti.combine = combine
+    oti = orc.TwoStageInverseFilterBankOracle(
+        lambda: orc.InverseFilterBankOracle(taps, 16, "8/7", 128, 16, "tukey"), nch2,
+        combine=combine)
+    rng = np.random.default_rng(22)
+    for n in (700, 450):
+        x = _noise(rng, (1, n_coarse * nch2, n))
+        ti, got = ti.execute(x)
+        ref = oti.execute(x)
+        assert_pfb_close(got, ref, what=f"two-stage inverse n={n}")
+
+
+# ----------------------------------------------------------------------------- harness
+def test_hip_backend_pipeline(gpu, tmp_path):
+    """generate -> channelize -> synthesize through DADA files, each step checked
+    against the oracle run on the data the previous step wrote."""
+    pfb = _pfb()
+    from ska_pst_dsp_model_amd import harness
+    taps = pfb.design_PFB_FIR_filter(8, "8/7", 10)
+    fir_path = tmp_path / "taps.txt"
+    np.savetxt(fir_path, taps[None, :])
+    run = harness.pipeline(
+        harness.partial(harness.generate_test_vector, domain_name="freq", n_bins=2688 + 704,
+                        n_pol=2),
+        harness.partial(harness.channelize, channels=8, os_factor_str="8/7",
+                        fir_filter_path=str(fir_path)),
+        harness.partial(harness.synthesize, input_fft_length=128, input_overlap=16,
+                        fft_window_str="tukey"),
+        output_dir=str(tmp_path))
+    tv, ch, sy = run(3, np.pi / 4)
+    x = tv.data.transpose(2, 1, 0)                                   # (pol, 1, t)
+    ref_chan = orc.polyphase_analysis(x, pfb.read_fir_filter_coeff(str(fir_path)), 8, "8/7")
+    assert_pfb_close(ch.data.transpose(2, 1, 0), ref_chan, what="channelize")
+    assert ch.header["OS_FACTOR"] == "8/7" and ch.header["NCHAN"] == "8"
+    assert ch.header["NTAP_0"] == str(len(taps)) and ch.header["PFB_DC_CHAN"] == "1"
+    hdr_taps = np.array([float(v) for v in ch.header["COEFF_0"].split(",")])
+    ref = orc.polyphase_synthesis(ch.data.transpose(2, 1, 0), 1, 128, "8/7",
+                                  {"apply_deripple": 1, "filter_coeff": hdr_taps}, 1, 16,
+                                  orc.pfb_window("tukey", 128, 16))
+    assert_pfb_close(sy.data.transpose(2, 1, 0), ref, what="synthesize")
+    assert sy.header["NCHAN"] == "1" and sy.header["NPOL"] == "2"
