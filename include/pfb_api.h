@@ -56,7 +56,10 @@ typedef enum pfb_status {
 
 typedef enum pfb_analysis_variant {
   PFB_ANALYSIS_BUNTON = 0, /* polyphase_analysis.m */
-  PFB_ANALYSIS_PADDED = 1  /* polyphase_analysis_padded.m */
+  PFB_ANALYSIS_PADDED = 1, /* polyphase_analysis_padded.m */
+  PFB_ANALYSIS_LOWCBF = 2  /* polyphase_analysis_lowcbf.m -> PSTFilterbank.m: the SKA-Low CBF
+                              PST filterbank (n_chan 256, os 4/3, 3072 taps fixed); 216
+                              output channels; 1536 zeros pre-padded on the plan's first call */
 } pfb_analysis_variant;
 
 typedef enum pfb_mem {
@@ -95,6 +98,10 @@ pfb_status pfb_analysis_plan_destroy(pfb_analysis_plan* plan);
  * Bunton K = floor((n_dat - P*N)/M) (polyphase_analysis.m:62), padded K = floor(n_dat/M)
  * (polyphase_analysis_padded.m:75). */
 int64_t pfb_analysis_output_length(const pfb_analysis_plan* plan, int64_t n_dat);
+
+/* Channels per output row: n_chan, or 216 for PFB_ANALYSIS_LOWCBF
+ * (polyphase_analysis_lowcbf.m:43, PSTFilterbank.m:44). */
+int32_t pfb_analysis_output_channels(const pfb_analysis_plan* plan);
 
 /* Stateless analysis — replaces polyphase_analysis(in, filt, block, os_factor) and
  * polyphase_analysis_padded(...).  in: n_pol series of n_dat samples; out: n_pol x

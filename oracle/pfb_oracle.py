@@ -823,3 +823,56 @@ def write_dada_data(data, nbit: int) -> np.ndarray:
         info = np.iinfo(t)
         inter = np.clip(matlab_round(np.nan_to_num(inter)), info.min, info.max)
     return inter.astype(t)
+
+
+# --------------------------------------------------------------------------- LowCBF PST
+def pst_filterbank_literal(din, fir_taps, do_padding: bool) -> np.ndarray:
+    """PSTFilterbank.m:1-46, statement by statement (float64, like the Matlab model):
+    returns dout (216, outputSamples)."""
+    nfilt = 3072
+    padding = 1536 if do_padding else 0
+    din = np.asarray(din).reshape(-1)
+    total = din.size + padding
+    n_out = (total - nfilt) // 192
+    dinp = np.zeros(total, dtype=np.complex128)
+    dinp[padding:padding + din.size] = din
+    h = np.asarray(fir_taps, dtype=np.float64).reshape(-1)
+    dout = np.zeros((216, max(n_out, 0)), dtype=np.complex128)
+    fft_in = np.zeros(256, dtype=np.complex128)
+    for k in range(max(n_out, 0)):
+        for n1 in range(256):  # :28-30, Matlab n1:256:end and n1:256:(n1+256*11)
+            fft_in[n1] = np.sum(h[n1::256] * dinp[k * 192 + n1:k * 192 + n1 + 256 * 11 + 1:256]) / 2**9
+        dout1 = np.fft.fftshift(np.fft.fft(fft_in)) / 128  # :35
+        rotation = np.mod(k * np.arange(-128, 128), 4)    # :41
+        dout2 = dout1 * np.exp(1j * 2 * np.pi * rotation / 4)
+        dout[:, k] = dout2[20:20 + 216]                     # :44, Matlab 21:(21+215)
+    return dout
+
+
+def polyphase_analysis_lowcbf(x, filt, block=256, os_factor="4/3", do_padding=True,
+                              literal=False) -> np.ndarray:
+    """polyphase_analysis_lowcbf.m:12-47: PSTFilterbank per polarisation, times
+    2^9 * 2048 * 256.  ``do_padding`` stands for the wrapper's ``persistent`` flag (true
+    on the first call of a session).  Vectorised over k unless ``literal``."""
+    x = _as_pnt(x)
+    n_pol = x.shape[0]
+    scale = 2**9 * 2048 * 256
+    outs = []
+    for p in range(n_pol):
+        if literal:
+            outs.append(pst_filterbank_literal(x[p], filt, do_padding) * scale)
+            continue
+        padding = 1536 if do_padding else 0
+        din = x[p].astype(np.complex128)
+        total = din.size + padding
+        n_out = max((total - 3072) // 192, 0)
+        dinp = np.concatenate([np.zeros(padding, dtype=np.complex128), din])
+        h = np.asarray(filt, dtype=np.float64).reshape(12, 256)        # h[m, n] = taps[n + 256 m]
+        idx = (np.arange(n_out)[:, None, None] * 192 + np.arange(12)[None, :, None] * 256 +
+               np.arange(256)[None, None, :])
+        u = np.einsum("kmn,mn->kn", dinp[idx], h) / 2**9 if n_out else np.zeros((0, 256))
+        F = np.fft.fftshift(np.fft.fft(u, axis=1), axes=1) / 128
+        rot = np.mod(np.arange(n_out)[:, None] * np.arange(-128, 128)[None, :], 4)
+        y = F * np.exp(1j * 2 * np.pi * rot / 4)
+        outs.append(y[:, 20:236].T * scale)
+    return np.stack(outs, axis=0)

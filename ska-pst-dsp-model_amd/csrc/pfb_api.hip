@@ -157,9 +157,17 @@ hipError_t copy_pols(float2* dst, int64_t dps, const float2* src, int64_t sps, i
 pfb_status pfb_set_error(pfb_status s, const char* msg) { return fail(s, "%s", msg); }
 
 // ====================================================================== analysis plan
+// LowCBF: every call consumes the one-time pre-padding (polyphase_analysis_lowcbf.m:27-34)
+struct PadConsume {
+  bool* flag;
+  ~PadConsume() { *flag = false; }
+};
+
 struct pfb_analysis_plan {
   int device = 0;
   int variant = 0, N = 0, nu = 1, de = 1, M = 0, P = 0, n_pol = 1, sds = 0;
+  int C = 0;                  // output channels per row (N; 216 for the LowCBF filterbank)
+  bool lowcbf_pad = false;    // LowCBF: the next call pre-pads 1536 zeros (persistent do_padding)
   int64_t n_taps = 0;
   bool fused = false;
   DevBuf taps, twN, scratch;
@@ -181,6 +189,23 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
                                int64_t K_total, hipStream_t s, float2* z = nullptr,
                                int64_t z_ps = 0, int64_t z_row0 = 0) {
   if (K_end <= row0) return PFB_OK;
+  if (p->variant == pfb::kLowCbf) {
+    pfb::LowCbfArgs l{};
+    l.in = in;
+    l.in_pol_stride = in_ps;
+    l.n_dat = n_dat;
+    l.pad = p->lowcbf_pad ? 1536 : 0;
+    l.out = out;
+    l.out_pol_stride = out_ps;
+    l.K = K_end;
+    l.n_pol = p->n_pol;
+    l.taps = p->taps.as<float>();
+    l.tw = p->twN.as<float2>();
+    l.scale = 4096.0f;  // 2^9 * 2048 * 256 / 2^9 / 128
+    ProfScope ps(0, (double)p->n_pol * (8.0 * n_dat + 8.0 * K_end * p->C), s);
+    HIPCHK(pfb::launch_lowcbf(l, s));
+    return PFB_OK;
+  }
   pfb::AnalysisArgs a{};
   a.z = z;
   a.z_pol_stride = z_ps;
@@ -231,6 +256,10 @@ static bool analysis_emits_z(const pfb_analysis_plan* p) {
 }
 
 static int64_t analysis_K(const pfb_analysis_plan* p, int64_t n_dat) {
+  if (p->variant == pfb::kLowCbf) {  // PSTFilterbank.m:14-15
+    const int64_t k = floordiv(n_dat + (p->lowcbf_pad ? 1536 : 0) - 3072, 192);
+    return std::max<int64_t>(k, 0);
+  }
   if (p->variant == pfb::kBunton) {
     const int64_t k = floordiv(n_dat - (int64_t)p->P * p->N, p->M);
     return std::max<int64_t>(k, 0);
@@ -252,7 +281,14 @@ int32_t pfb_device_count(void) {
 pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_plan** out) {
   if (!d || !out) return fail(PFB_ERR_INVALID_ARG, "null argument");
   *out = nullptr;
-  if (d->variant != PFB_ANALYSIS_BUNTON && d->variant != PFB_ANALYSIS_PADDED)
+  if (d->variant == PFB_ANALYSIS_LOWCBF &&
+      (d->n_chan != 256 || d->os_nu != 4 || d->os_de != 3 || d->n_taps != 3072))
+    return fail(PFB_ERR_INVALID_ARG,
+                "polyphase_analysis_lowcbf is the fixed 256-channel 4/3 PST filterbank with "
+                "3072 taps (PSTFilterbank.m:7-15); got n_chan=%d os=%d/%d taps=%lld",
+                d->n_chan, d->os_nu, d->os_de, (long long)d->n_taps);
+  if (d->variant != PFB_ANALYSIS_BUNTON && d->variant != PFB_ANALYSIS_PADDED &&
+      d->variant != PFB_ANALYSIS_LOWCBF)
     return fail(PFB_ERR_INVALID_ARG, "unknown analysis variant %d", d->variant);
   if (d->n_chan <= 0 || d->os_nu <= 0 || d->os_de <= 0 || d->os_de > d->os_nu)
     return fail(PFB_ERR_INVALID_ARG, "invalid n_chan/os_factor (%d, %d/%d)", d->n_chan, d->os_nu,
@@ -279,7 +315,12 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
     delete p;
     return fail(PFB_ERR_INVALID_ARG, "commutator step M = floor(N de/nu) is zero");
   }
-  if (!pfb::analysis_supported(p->N, p->P, p->variant, &p->fused)) {
+  p->C = p->N;
+  if (p->variant == pfb::kLowCbf) {
+    p->C = 216;
+    p->lowcbf_pad = true;
+    p->fused = true;
+  } else if (!pfb::analysis_supported(p->N, p->P, p->variant, &p->fused)) {
     delete p;
     return fail(PFB_ERR_UNSUPPORTED, "no analysis kernel for n_chan=%d", d->n_chan);
   }
@@ -316,6 +357,8 @@ pfb_status pfb_analysis_plan_destroy(pfb_analysis_plan* p) {
   return PFB_OK;
 }
 
+int32_t pfb_analysis_output_channels(const pfb_analysis_plan* p) { return p ? p->C : -1; }
+
 int64_t pfb_analysis_output_length(const pfb_analysis_plan* p, int64_t n_dat) {
   if (!p) return -1;
   return analysis_K(p, n_dat);
@@ -329,25 +372,26 @@ pfb_status pfb_analysis_execute(pfb_analysis_plan* p, const pfb_cf32* in, int64_
   HIPCHK(hipSetDevice(p->device));
   hipStream_t s = (hipStream_t)stream;
   const int64_t K = analysis_K(p, n_dat);
+  PadConsume pad_once{&p->lowcbf_pad};
   if (n_out) *n_out = K;
   if (K == 0) return PFB_OK;
   if (!out) return fail(PFB_ERR_INVALID_ARG, "null output");
   if (cap < K) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld rows",
                            (long long)cap, (long long)K);
   if (mem == PFB_MEM_DEVICE) {
-    if (in_ps < n_dat || out_ps < K * p->N)
+    if (in_ps < n_dat || out_ps < K * p->C)
       return fail(PFB_ERR_INVALID_ARG, "polarisation stride smaller than the data");
     return analysis_run(p, (const float2*)in, in_ps, n_dat, (float2*)out, out_ps, 0, K, K, s);
   }
   // host staging (synchronous)
   HIPCHK(p->stage_in.ensure((size_t)p->n_pol * n_dat * sizeof(float2)));
-  HIPCHK(p->stage_out.ensure((size_t)p->n_pol * K * p->N * sizeof(float2)));
+  HIPCHK(p->stage_out.ensure((size_t)p->n_pol * K * p->C * sizeof(float2)));
   HIPCHK(copy_pols(p->stage_in.as<float2>(), n_dat, (const float2*)in, in_ps, n_dat, p->n_pol,
                    hipMemcpyHostToDevice, s));
   pfb_status st = analysis_run(p, p->stage_in.as<float2>(), n_dat, n_dat,
-                               p->stage_out.as<float2>(), K * p->N, 0, K, K, s);
+                               p->stage_out.as<float2>(), K * p->C, 0, K, K, s);
   if (st != PFB_OK) return st;
-  HIPCHK(copy_pols((float2*)out, out_ps, p->stage_out.as<float2>(), K * p->N, K * p->N, p->n_pol,
+  HIPCHK(copy_pols((float2*)out, out_ps, p->stage_out.as<float2>(), K * p->C, K * p->C, p->n_pol,
                    hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   return PFB_OK;
@@ -368,6 +412,7 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
                    hipMemcpyDeviceToDevice, s));
   HIPCHK(copy_pols(w + p->buffered, total, (const float2*)in, in_ps, n_in, p->n_pol, kin, s));
   const int64_t K = analysis_K(p, total);
+  PadConsume pad_once{&p->lowcbf_pad};
   const int64_t Kt = K - (K % p->nu);  // trim to a multiple of nu (FilterBank.m:93-104)
   if (n_out) *n_out = Kt;
   if (Kt > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld rows",
@@ -376,23 +421,23 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
     float2* dst;
     int64_t dps;
     if (mem == PFB_MEM_HOST) {
-      HIPCHK(p->stage_out.ensure((size_t)p->n_pol * K * p->N * sizeof(float2)));
+      HIPCHK(p->stage_out.ensure((size_t)p->n_pol * K * p->C * sizeof(float2)));
       dst = p->stage_out.as<float2>();
-      dps = K * p->N;
+      dps = K * p->C;
     } else {
       dst = (float2*)out;
       dps = out_ps;
       if (Kt != K) {  // kernels write K rows; stage when the caller sized for Kt only
-        HIPCHK(p->stage_out.ensure((size_t)p->n_pol * K * p->N * sizeof(float2)));
+        HIPCHK(p->stage_out.ensure((size_t)p->n_pol * K * p->C * sizeof(float2)));
         dst = p->stage_out.as<float2>();
-        dps = K * p->N;
+        dps = K * p->C;
       }
     }
     pfb_status st = analysis_run(p, w, total, total, dst, dps, 0, K, K, s);
     if (st != PFB_OK) return st;
     if (dst != (float2*)out) {
       const hipMemcpyKind ko = mem == PFB_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
-      HIPCHK(copy_pols((float2*)out, out_ps, dst, dps, Kt * p->N, p->n_pol, ko, s));
+      HIPCHK(copy_pols((float2*)out, out_ps, dst, dps, Kt * p->C, p->n_pol, ko, s));
     }
   }
   // carry = input(:,:,input_idat+1:end), input_idat = T_out N de / nu   (FilterBank.m:119-126)
@@ -414,6 +459,7 @@ int64_t pfb_filterbank_buffered(const pfb_analysis_plan* p) { return p ? p->buff
 pfb_status pfb_filterbank_reset(pfb_analysis_plan* p) {
   if (!p) return fail(PFB_ERR_INVALID_ARG, "null plan");
   p->buffered = 0;
+  p->lowcbf_pad = p->variant == pfb::kLowCbf;
   return PFB_OK;
 }
 
@@ -863,6 +909,8 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
                                  void* stream) {
   if (!pa || !ps || (!in && n_dat > 0)) return fail(PFB_ERR_INVALID_ARG, "null argument");
   if (pa->device != ps->device) return fail(PFB_ERR_INVALID_ARG, "plans on different devices");
+  if (pa->variant == pfb::kLowCbf)
+    return fail(PFB_ERR_UNSUPPORTED, "round trip of the LowCBF filterbank: use the separate calls");
   if (pa->N != ps->N || pa->n_pol != ps->n_pol)
     return fail(PFB_ERR_INVALID_ARG, "analysis (%d ch, %d pol) and synthesis (%d ch, %d pol) differ",
                 pa->N, pa->n_pol, ps->N, ps->n_pol);

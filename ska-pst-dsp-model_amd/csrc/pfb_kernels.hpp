@@ -7,7 +7,7 @@
 
 namespace pfb {
 
-enum Variant { kBunton = 0, kPadded = 1 };
+enum Variant { kBunton = 0, kPadded = 1, kLowCbf = 2 };
 
 // Polyphase analysis (polyphase_analysis.m / polyphase_analysis_padded.m).
 struct AnalysisArgs {
@@ -76,6 +76,23 @@ struct SynthBlockArgs {
   int timing_mask;         // timing experiments only (PFB_TIMING_MASK): bit0 drop Z loads,
                            // bit1 drop output stores, bit2 drop tw4 loads (results invalid)
 };
+
+// SKA-Low CBF PST filterbank (polyphase_analysis_lowcbf.m / PSTFilterbank.m):
+// 256 arms x 12 taps, step 192, forward FFT, fftshift, pi/2 derotation, 216 channels.
+struct LowCbfArgs {
+  const float2* in;        // [pol][t]
+  int64_t in_pol_stride;
+  int64_t n_dat;
+  int64_t pad;             // leading zeros (1536 on the first call, else 0)
+  float2* out;             // [pol][k][216]
+  int64_t out_pol_stride;
+  int64_t K;
+  int n_pol;
+  const float* taps;       // 3072 taps (device)
+  const float2* tw;        // e^{-2 pi i m / 256}
+  float scale;             // 2^28 / 2^9 / 128 = 2^12
+};
+hipError_t launch_lowcbf(const LowCbfArgs& a, hipStream_t s);
 
 bool analysis_supported(int N, int P, int variant, bool* fused);
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s);

@@ -10,6 +10,7 @@ kernels of ``lib/libpfb_hip.so`` (C ABI: ``include/pfb_api.h``).
 from ._lib import PfbError, device_count
 from .config import Rational, default_config, load_config
 from .core import (AnalysisPlan, SynthesisPlan, polyphase_analysis, polyphase_analysis_padded,
+                   polyphase_analysis_lowcbf,
                    polyphase_synthesis, roundtrip)
 from .filterbank import (Channelizer, DeChannelizer, FilterBank, InverseFilterBank,
                          TwoStageFilterBank, TwoStageInverseFilterBank)
@@ -20,7 +21,7 @@ from . import dada, harness, layout, sharding
 
 __all__ = [
     "PfbError", "device_count", "Rational", "default_config", "load_config", "AnalysisPlan",
-    "SynthesisPlan", "polyphase_analysis", "polyphase_analysis_padded", "polyphase_synthesis",
+    "SynthesisPlan", "polyphase_analysis", "polyphase_analysis_padded", "polyphase_analysis_lowcbf", "polyphase_synthesis",
     "Channelizer", "DeChannelizer", "FilterBank", "InverseFilterBank", "TwoStageFilterBank",
     "TwoStageInverseFilterBank", "design_PFB_FIR_filter", "design_PFB_FIR_filter_two_stage",
     "read_fir_filter_coeff", "PFBWindow", "identity_taper", "roundtrip",

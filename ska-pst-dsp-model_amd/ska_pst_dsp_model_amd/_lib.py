@@ -26,6 +26,7 @@ PFB_ERR_NO_DEVICE = 6
 
 PFB_ANALYSIS_BUNTON = 0
 PFB_ANALYSIS_PADDED = 1
+PFB_ANALYSIS_LOWCBF = 2
 PFB_MEM_DEVICE = 0
 PFB_MEM_HOST = 1
 
@@ -73,6 +74,7 @@ SYMBOLS = [
     ("pfb_analysis_plan_create", c_int32, [POINTER(AnalysisDesc), POINTER(c_void_p)]),
     ("pfb_analysis_plan_destroy", c_int32, [c_void_p]),
     ("pfb_analysis_output_length", c_int64, [c_void_p, c_int64]),
+    ("pfb_analysis_output_channels", c_int32, [c_void_p]),
     ("pfb_analysis_execute", c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64,
                                        c_int64, POINTER(c_int64), c_int32, c_void_p]),
     ("pfb_filterbank_execute", c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64,

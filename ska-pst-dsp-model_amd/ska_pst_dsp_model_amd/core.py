@@ -28,6 +28,7 @@ from .config import Rational, as_rational
 from .window import PFBWindow, Taper, identity_taper
 
 __all__ = ["AnalysisPlan", "SynthesisPlan", "polyphase_analysis", "polyphase_analysis_padded",
+           "polyphase_analysis_lowcbf",
            "polyphase_synthesis", "analysis_plan", "synthesis_plan", "is_device_array",
            "roundtrip"]
 
@@ -71,7 +72,9 @@ class AnalysisPlan:
         self.variant = variant
         v = {"polyphase_analysis": _lib.PFB_ANALYSIS_BUNTON, "bunton": _lib.PFB_ANALYSIS_BUNTON,
              "polyphase_analysis_padded": _lib.PFB_ANALYSIS_PADDED,
-             "padded": _lib.PFB_ANALYSIS_PADDED}
+             "padded": _lib.PFB_ANALYSIS_PADDED,
+             "polyphase_analysis_lowcbf": _lib.PFB_ANALYSIS_LOWCBF,
+             "lowcbf": _lib.PFB_ANALYSIS_LOWCBF}
         if variant not in v:
             raise ValueError(f"unknown analysis function '{variant}'")
         self.taps = _taps64(taps)
@@ -82,6 +85,7 @@ class AnalysisPlan:
         _lib.check(lib.pfb_analysis_plan_create(byref(d), byref(h)))
         self._h = h
         self._lib = lib
+        self.out_chan = int(lib.pfb_analysis_output_channels(h))  # 216 for LowCBF
         self.step = (self.n_chan * self.os_factor.de) // self.os_factor.nu
         self.phases = -(-len(self.taps) // self.n_chan)
 
@@ -128,9 +132,9 @@ class AnalysisPlan:
     def _alloc_out(self, like, dev, rows):
         if dev:
             t = _torch()
-            return t.empty((self.n_pol, max(rows, 0), self.n_chan), dtype=t.complex64,
+            return t.empty((self.n_pol, max(rows, 0), self.out_chan), dtype=t.complex64,
                            device=like.device)
-        return np.empty((self.n_pol, max(rows, 0), self.n_chan), dtype=np.complex64)
+        return np.empty((self.n_pol, max(rows, 0), self.out_chan), dtype=np.complex64)
 
     def execute(self, x, stateful: bool = False):
         """Run the analysis; returns the (n_pol, K, n_chan) buffer (time-major)."""
@@ -151,7 +155,7 @@ class AnalysisPlan:
             src, dst, mem, stream = x.ctypes.data_as(c_void_p), out.ctypes.data_as(c_void_p), \
                 _lib.PFB_MEM_HOST, c_void_p(0)
         fn = self._lib.pfb_filterbank_execute if stateful else self._lib.pfb_analysis_execute
-        _lib.check(fn(self._h, src, n_dat, n_dat, dst, cap * self.n_chan, cap, byref(n_out),
+        _lib.check(fn(self._h, src, n_dat, n_dat, dst, cap * self.out_chan, cap, byref(n_out),
                       mem, stream))
         return out[:, :n_out.value, :]
 
@@ -410,6 +414,15 @@ def polyphase_analysis(in_, filt, block, os_factor, verbose_=0):
 def polyphase_analysis_padded(in_, filt, block, os_factor, verbose_=0):
     """polyphase_analysis_padded.m:1-161 (commutator).  Returns (n_pol, block, nblocks)."""
     plan = analysis_plan(filt, block, os_factor, "polyphase_analysis_padded", _npol(in_),
+                         _device_of(in_))
+    return _pfc_view(plan.execute(in_))
+
+
+def polyphase_analysis_lowcbf(in_, filt, block=256, os_factor="4/3", verbose_=0):
+    """polyphase_analysis_lowcbf.m:1-49 (SKA-Low CBF PST filterbank, PSTFilterbank.m).
+    Returns (n_pol, 216, nblocks).  The wrapper's ``persistent do_padding`` (1536 zeros
+    before the first call's data only) lives in the cached plan of these taps."""
+    plan = analysis_plan(filt, 256, "4/3", "polyphase_analysis_lowcbf", _npol(in_),
                          _device_of(in_))
     return _pfc_view(plan.execute(in_))
 

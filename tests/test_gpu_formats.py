@@ -246,3 +246,61 @@ def test_hip_backend_pipeline(gpu, tmp_path):
                                   orc.pfb_window("tukey", 128, 16))
     assert_pfb_close(sy.data.transpose(2, 1, 0), ref, what="synthesize")
     assert sy.header["NCHAN"] == "1" and sy.header["NPOL"] == "2"
+
+
+# ----------------------------------------------------------------------------- LowCBF PST
+def _pst_taps():
+    pfb = _pfb()
+    return pfb.read_fir_filter_coeff(pfb.config.config_dir + "/PST_filtertaps.txt")
+
+
+def test_lowcbf_matches_oracle_and_pads_once(gpu):
+    """polyphase_analysis_lowcbf: 1536-zero pre-padding on the plan's first call only
+    (the wrapper's persistent do_padding), 216 kept channels, 2^12 net scale."""
+    pfb = _pfb()
+    taps = _pst_taps()
+    rng = np.random.default_rng(71)
+    plan = pfb.AnalysisPlan(taps, 256, "4/3", "polyphase_analysis_lowcbf", 2)
+    assert plan.out_chan == 216
+    for call, n in enumerate((1 << 16, 50001, 3000)):
+        x = _noise(rng, (2, 1, n))
+        got = plan.execute(x).transpose(0, 2, 1)
+        ref = orc.polyphase_analysis_lowcbf(x, taps, do_padding=(call == 0))
+        assert got.shape == ref.shape, (got.shape, ref.shape)
+        if ref.size:
+            assert_pfb_close(got, ref, what=f"lowcbf call {call}")
+    plan.reset()
+    x = _noise(rng, (2, 1, 20000))
+    assert_pfb_close(plan.execute(x).transpose(0, 2, 1),
+                     orc.polyphase_analysis_lowcbf(x, taps, do_padding=True), what="after reset")
+
+
+def test_lowcbf_filterbank_stream(gpu):
+    """FilterBank with analysis_function polyphase_analysis_lowcbf (config lowpsi):
+    nu-trim to multiples of 4 and the 192-sample carry, as FilterBank.m does."""
+    pfb = _pfb()
+    taps = _pst_taps()
+    cfg = dict(analysis_function="polyphase_analysis_lowcbf", filt_coeff=taps, channels=256,
+               os_factor="4/3")
+    fb = pfb.FilterBank(cfg)
+
+    class _LowCbfOracle(orc.FilterBankOracle):
+        def __init__(self):
+            super().__init__(taps, 256, "4/3")
+            self.first = True
+            self.pfb_analysis = self._call
+
+        def _call(self, x, filt, n_chan, os_factor):
+            y = orc.polyphase_analysis_lowcbf(x, filt, do_padding=self.first)
+            self.first = False
+            return y
+
+    ofb = _LowCbfOracle()
+    rng = np.random.default_rng(72)
+    for n in (30000, 12345, 40000):
+        x = _noise(rng, (1, 1, n))
+        fb, got = fb.execute(x)
+        ref = ofb.execute(x)
+        assert got.shape == ref.shape, (got.shape, ref.shape)
+        assert_pfb_close(got, ref, what=f"lowcbf stream n={n}")
+        assert fb.buffered_samples == ofb.buffered_samples

@@ -226,3 +226,32 @@ def test_oracle_matches_committed_golden(name):
                                 {"apply_deripple": 1, "filter_coeff": taps}, 1, int(g["ov"]),
                                 orc.pfb_window("tukey", int(g["nf"]), int(g["ov"])))
     assert_pfb_close(y, g["y"], tol=1e-6)
+
+
+@pytest.mark.parametrize("do_padding", [True, False])
+def test_lowcbf_vectorised_equals_literal(do_padding):
+    """polyphase_analysis_lowcbf: vectorised restatement == the PSTFilterbank.m loop."""
+    import ska_pst_dsp_model_amd as pfb
+    taps = pfb.read_fir_filter_coeff(pfb.config.config_dir + "/PST_filtertaps.txt")
+    assert taps.size == 3072
+    rng = np.random.default_rng(61)
+    x = (rng.standard_normal((2, 1, 3072 + 192 * 9 + 77)) +
+         1j * rng.standard_normal((2, 1, 3072 + 192 * 9 + 77)))
+    a = orc.polyphase_analysis_lowcbf(x, taps, do_padding=do_padding)
+    b = orc.polyphase_analysis_lowcbf(x, taps, do_padding=do_padding, literal=True)
+    assert a.shape == (2, 216, 9 + (8 if do_padding else 0))
+    assert np.allclose(a, b, rtol=1e-12, atol=1e-9 * np.abs(b).max())
+
+
+def test_lowcbf_tone_lands_in_its_channel():
+    """A tone at fine-channel centre c (SKA-Low PST: 256-pt FFT at 4/3, DC at 129)
+    concentrates in output channel c - 20 + 128 of the 216 kept."""
+    import ska_pst_dsp_model_amd as pfb
+    taps = pfb.read_fir_filter_coeff(pfb.config.config_dir + "/PST_filtertaps.txt")
+    n = 3072 + 192 * 63
+    f = 10  # bins of 1/256 cycles per sample
+    x = np.exp(2j * np.pi * f / 256 * np.arange(n))[None, None, :]
+    y = orc.polyphase_analysis_lowcbf(x, taps, do_padding=False)
+    power = (np.abs(y) ** 2).mean(axis=2)[0]
+    assert int(np.argmax(power)) == f + 128 - 20
+    assert power.max() > 1e3 * np.sort(power)[-3]
