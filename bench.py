@@ -53,6 +53,10 @@ def parse():
                          "analysis and synthesis calls")
     ap.add_argument("--kernel-events", type=int, default=1,
                     help="record HIP events around every kernel in the timed region")
+    ap.add_argument("--e2e", type=int, default=0,
+                    help="also time the host-buffer path: pinned DADA bytes (NBIT 8 TFP) -> "
+                         "H2D -> unpack -> round trip -> pack (NBIT 32) -> D2H (reported as "
+                         "e2e_pcie; never the headline value)")
     return ap.parse_args()
 
 
@@ -95,6 +99,39 @@ def pmc_traffic():
             return json.load(f)
     except Exception:
         return None
+
+
+def e2e_pcie(torch, dev, pfb, ana, syn, n_pol, n_dat, chan_buf, out_buf, steps, world, dist):
+    """Host-buffer rate of the DADA path: int8 TFP bytes in pinned host
+    memory -> H2D -> pfb_dada_unpack -> round trip -> pfb_dada_pack (float32) -> D2H into
+    pinned memory, one unit per step, serial on one stream."""
+    from ska_pst_dsp_model_amd import layout
+    rng = np.random.default_rng(5)
+    raw_h = torch.from_numpy(rng.integers(-40, 40, size=n_dat * n_pol * 2, dtype=np.int8)
+                             .view(np.uint8)).pin_memory()
+    n_out = out_buf.shape[1]
+    res_h = torch.empty((n_out * n_pol * 2,), dtype=torch.float32).pin_memory()
+    raw_d = torch.empty_like(raw_h, device=dev)
+
+    def step():
+        raw_d.copy_(raw_h, non_blocking=True)
+        x = layout.dada_unpack(raw_d, 8, 2, 1, n_pol)[:, :, 0]       # (n_pol, n_dat)
+        pfb.roundtrip(ana, syn, x, chan=chan_buf, out=out_buf)
+        packed = layout.dada_pack(out_buf[:, :, None], 32)
+        res_h.copy_(packed, non_blocking=True)
+
+    step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    return {"value": round(n_pol * n_dat * steps / el / 1e6, 2), "unit": "complex Msamples/s",
+            "per_gpu": True, "input": "DADA NBIT 8 TFP, pinned host memory",
+            "output": "DADA NBIT 32 TFP, pinned host memory", "ms_per_step": round(el / steps * 1e3, 3)}
 
 
 def main():
@@ -202,6 +239,11 @@ def main():
                               "alg_bytes_per_launch": by.value / nl.value,
                               "ms_per_step": ms.value / args.steps}
 
+    e2e = None
+    if args.e2e:
+        e2e = e2e_pcie(torch, dev, pfb, ana, syn, n_pol, n_dat, chan_buf, out_buf, args.steps,
+                       world, dist)
+
     if rank == 0:
         samples = world * n_pol * n_dat * args.steps
         value = samples / el / 1e6
@@ -244,6 +286,8 @@ def main():
             "ms_per_step_with_kernel_events": round(el_prof / args.steps * 1e3, 4),
             "kernels": kern,
         }
+        if e2e is not None:
+            out["e2e_pcie"] = e2e
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(taps, args.cpu_seconds)
         else:

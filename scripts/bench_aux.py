@@ -1,0 +1,133 @@
+"""Secondary measurements (not the bench.py headline): every other kernel of the path on
+one MI355X, as algorithmic HBM bytes / time against the 8 TB/s peak.
+
+  * C3 SKA-Mid padded round trip (4096 ch, 8/7, 100 353 taps, 2^26 samples)
+  * C2' reference 'low' parity variant (256 ch, 4/3)
+  * LowCBF PST filterbank (polyphase_analysis_lowcbf, 2^24 samples x 2 pol)
+  * DADA unpack (NBIT 8 / 32) and pack, corner turn, channel gather, quantisation
+  * two-stage analysis cascade (256 x 256 ch; stage 2 batched over 256 series)
+
+Prints one JSON object per line.  Usage: python scripts/bench_aux.py [--reps N]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "ska-pst-dsp-model_amd"), REPO]
+PEAK = 8000.0
+
+
+def timeit(torch, fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def emit(name, ms, alg_bytes, **kw):
+    gbs = alg_bytes / (ms * 1e-3) / 1e9
+    print(json.dumps({"kernel": name, "ms": round(ms, 4), "alg_bytes": int(alg_bytes),
+                      "GB/s": round(gbs, 1), "frac": round(gbs / PEAK, 4), **kw}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--skip-mid", action="store_true")
+    args = ap.parse_args()
+    import torch
+    import ska_pst_dsp_model_amd as pfb
+    from ska_pst_dsp_model_amd import layout
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(1)
+
+    def noise(*shape):
+        return torch.complex(torch.randn(shape, device=dev, generator=g),
+                             torch.randn(shape, device=dev, generator=g)).to(torch.complex64)
+
+    # ---- C2' (4/3) round trip
+    taps43 = pfb.design_PFB_FIR_filter(256, "4/3", 12)
+    n = 1 << 24
+    x = noise(1, n)
+    ana = pfb.AnalysisPlan(taps43, 256, "4/3", "polyphase_analysis", 1)
+    win = pfb.PFBWindow().lookup["tukey"](256, 48)
+    syn = pfb.SynthesisPlan(256, "4/3", 256, 48, True, 1, True, taps43, win, None, 1)
+    K = ana.output_length(n)
+    chan = torch.empty((1, K, 256), dtype=torch.complex64, device=dev)
+    out = torch.empty((1, syn.output_length(K)), dtype=torch.complex64, device=dev)
+    ms = timeit(torch, lambda: pfb.roundtrip(ana, syn, x, chan=chan, out=out), args.reps)
+    emit("roundtrip C2' 256ch 4/3", ms, 16 * (1 + 4 / 3) * n,
+         msamples_per_s=round(n / ms / 1e3, 1))
+
+    # ---- LowCBF PST filterbank
+    taps_pst = pfb.read_fir_filter_coeff(os.path.join(pfb.config.config_dir, "PST_filtertaps.txt"))
+    x2 = noise(2, n)
+    low = pfb.AnalysisPlan(taps_pst, 256, "4/3", "polyphase_analysis_lowcbf", 2)
+    low.execute(x2)  # consume the one-time padding
+    Kl = low.output_length(n)
+    ms = timeit(torch, lambda: low.execute(x2), args.reps)
+    emit("lowcbf_kernel (PSTFilterbank)", ms, 2 * (8 * n + 8 * 216 * Kl),
+         msamples_per_s=round(2 * n / ms / 1e3, 1))
+
+    # ---- layout kernels
+    raw8 = torch.randint(-128, 127, (2 * 2 * n,), dtype=torch.int8, device=dev)
+    ms = timeit(torch, lambda: layout.dada_unpack(raw8, 8, 2, 1, 2), args.reps)
+    emit("dada_unpack NBIT8 2pol", ms, raw8.numel() + 2 * n * 8)
+    raw32 = torch.randn((2 * 2 * n,), device=dev)
+    ms = timeit(torch, lambda: layout.dada_unpack(raw32, 32, 2, 1, 2), args.reps)
+    emit("dada_unpack NBIT32 2pol", ms, raw32.numel() * 4 + 2 * n * 8)
+    y = noise(2, n, 1)
+    ms = timeit(torch, lambda: layout.dada_pack(y, 32), args.reps)
+    emit("dada_pack NBIT32 2pol", ms, 2 * 2 * n * 8)
+    rows = noise(1 << 16, 256)
+    ms = timeit(torch, lambda: layout.corner_turn(rows), args.reps)
+    emit("corner_turn 65536x256", ms, 2 * rows.numel() * 8)
+    ms = timeit(torch, lambda: layout.gather_channels(rows, 16, 16, 256, 1 << 16, 16), args.reps)
+    emit("gather_channels 16x16", ms, 2 * rows.numel() * 8)
+    ms = timeit(torch, lambda: layout.quantize(y, 33.8), args.reps)
+    emit("quantize (moments + round)", ms, 3 * y.numel() * 8)
+
+    # ---- two-stage analysis: 256 ch, then 256 ch over each (batched)
+    taps87 = pfb.design_PFB_FIR_filter(256, "8/7", 12)
+    cfg = dict(analysis_function="polyphase_analysis", filt_coeff=taps87, channels=256,
+               os_factor="8/7")
+    ts = pfb.TwoStageFilterBank(cfg)
+    xs = noise(1, 1, 1 << 24)
+    ts.execute(xs)
+    ts2 = pfb.TwoStageFilterBank(cfg)
+    ms = timeit(torch, lambda: ts2.execute(xs), 3)
+    emit("TwoStageFilterBank 256x256 (stream call)", ms, 16 * (1 + 8 / 7) * (1 << 24),
+         msamples_per_s=round((1 << 24) / ms / 1e3, 1),
+         note="bytes: the two analyses' input+output, excluding the corner turn")
+
+    # ---- C3 SKA-Mid padded round trip
+    if not args.skip_mid:
+        del x, x2, raw8, raw32, y, rows, chan, out
+        torch.cuda.empty_cache()
+        tm = pfb.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
+        nm = 1 << 26
+        xm = noise(1, nm)
+        anam = pfb.AnalysisPlan(tm, 4096, "8/7", "polyphase_analysis_padded", 1)
+        winm = pfb.PFBWindow().lookup["tukey"](512, 128)
+        synm = pfb.SynthesisPlan(4096, "8/7", 512, 128, True, 1, True, tm, winm, None, 1)
+        Km = anam.output_length(nm)
+        chm = torch.empty((1, Km, 4096), dtype=torch.complex64, device=dev)
+        om = torch.empty((1, synm.output_length(Km)), dtype=torch.complex64, device=dev)
+        ms = timeit(torch, lambda: pfb.roundtrip(anam, synm, xm, chan=chm, out=om), 3)
+        emit("roundtrip C3 SKA-Mid padded 4096ch", ms, 16 * (1 + 8 / 7) * nm,
+             msamples_per_s=round(nm / ms / 1e3, 1), n_taps=len(tm))
+
+
+if __name__ == "__main__":
+    main()

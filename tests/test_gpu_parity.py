@@ -115,14 +115,30 @@ def test_analysis_many_taps_fused(gpu, N, os_, ppc):
     assert_pfb_close(got, ref)
 
 
-def test_analysis_generic_path(gpu):
-    """N > 256 goes through the FIR + row-FFT kernels."""
+@pytest.mark.parametrize("N,os_,ppc,variant", [
+    (512, "8/7", 12, "bunton"),    # register-window FIR, PW 13, DE 7
+    (512, "4/3", 12, "padded"),    # PW 13, DE 3
+    (1024, "4/3", 24, "bunton"),   # PW 25
+    (512, "8/7", 19, "padded"),    # PW 25 (P 20)
+    (512, "8/7", 28, "bunton"),    # PW 32 (P 29)
+    (512, "32/27", 12, "padded"),  # DE 27
+    (768, "8/7", 12, "bunton"),    # no row-FFT size for 768 -> rejected at plan time
+])
+def test_analysis_generic_path(gpu, N, os_, ppc, variant):
+    """N > 256 goes through the FIR (register-window kernel) + row-FFT kernels, two
+    polarisations, an input length that is not a multiple of anything."""
     import torch
     pfb = _pfb()
-    taps = pfb.design_PFB_FIR_filter(512, "8/7", 12)
-    x = _noise(np.random.default_rng(5), (1, 1, 60000))
-    ref = orc.polyphase_analysis(x, taps, 512, "8/7")
-    got = pfb.polyphase_analysis(torch.from_numpy(x).to(gpu), taps, 512, "8/7").cpu().numpy()
+    taps = pfb.design_PFB_FIR_filter(N, os_, ppc)
+    x = _noise(np.random.default_rng(5), (2, 1, 60000 + 37))
+    fn_o = orc.polyphase_analysis if variant == "bunton" else orc.polyphase_analysis_padded
+    fn_g = pfb.polyphase_analysis if variant == "bunton" else pfb.polyphase_analysis_padded
+    if N == 768:
+        with pytest.raises(pfb.PfbError):
+            fn_g(torch.from_numpy(x).to(gpu), taps, N, os_)
+        return
+    ref = fn_o(x, taps, N, os_)
+    got = fn_g(torch.from_numpy(x).to(gpu), taps, N, os_).cpu().numpy()
     assert_pfb_close(got, ref)
 
 
