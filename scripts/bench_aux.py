@@ -45,6 +45,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--skip-mid", action="store_true")
+    ap.add_argument("--only-mid", action="store_true")
     args = ap.parse_args()
     import torch
     import ska_pst_dsp_model_amd as pfb
@@ -56,6 +57,8 @@ def main():
         return torch.complex(torch.randn(shape, device=dev, generator=g),
                              torch.randn(shape, device=dev, generator=g)).to(torch.complex64)
 
+    if args.only_mid:
+        return mid(torch, pfb, noise, dev)
     # ---- C2' (4/3) round trip
     taps43 = pfb.design_PFB_FIR_filter(256, "4/3", 12)
     n = 1 << 24
@@ -115,18 +118,22 @@ def main():
     if not args.skip_mid:
         del x, x2, raw8, raw32, y, rows, chan, out
         torch.cuda.empty_cache()
-        tm = pfb.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
-        nm = 1 << 26
-        xm = noise(1, nm)
-        anam = pfb.AnalysisPlan(tm, 4096, "8/7", "polyphase_analysis_padded", 1)
-        winm = pfb.PFBWindow().lookup["tukey"](512, 128)
-        synm = pfb.SynthesisPlan(4096, "8/7", 512, 128, True, 1, True, tm, winm, None, 1)
-        Km = anam.output_length(nm)
-        chm = torch.empty((1, Km, 4096), dtype=torch.complex64, device=dev)
-        om = torch.empty((1, synm.output_length(Km)), dtype=torch.complex64, device=dev)
-        ms = timeit(torch, lambda: pfb.roundtrip(anam, synm, xm, chan=chm, out=om), 3)
-        emit("roundtrip C3 SKA-Mid padded 4096ch", ms, 16 * (1 + 8 / 7) * nm,
-             msamples_per_s=round(nm / ms / 1e3, 1), n_taps=len(tm))
+        mid(torch, pfb, noise, dev)
+
+
+def mid(torch, pfb, noise, dev, reps=3):
+    tm = pfb.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
+    nm = 1 << 26
+    xm = noise(1, nm)
+    anam = pfb.AnalysisPlan(tm, 4096, "8/7", "polyphase_analysis_padded", 1)
+    winm = pfb.PFBWindow().lookup["tukey"](512, 128)
+    synm = pfb.SynthesisPlan(4096, "8/7", 512, 128, True, 1, True, tm, winm, None, 1)
+    Km = anam.output_length(nm)
+    chm = torch.empty((1, Km, 4096), dtype=torch.complex64, device=dev)
+    om = torch.empty((1, synm.output_length(Km)), dtype=torch.complex64, device=dev)
+    ms = timeit(torch, lambda: pfb.roundtrip(anam, synm, xm, chan=chm, out=om), reps)
+    emit("roundtrip C3 SKA-Mid padded 4096ch", ms, 16 * (1 + 8 / 7) * nm,
+         msamples_per_s=round(nm / ms / 1e3, 1), n_taps=len(tm))
 
 
 if __name__ == "__main__":

@@ -476,6 +476,7 @@ struct pfb_synthesis_plan {
   int timing_mask = 0;  // PFB_TIMING_MASK (timing experiments; results invalid when set)
   int ranges = -1;  // PFB_SYNTH_RANGES: 0 one workgroup per block, -1 persistent auto, >0 persistent
   int no_reuse = 0;  // PFB_SYNTH_NO_REUSE: re-read the overlap rows (A/B measurement only)
+  int xcd = 1;       // PFB_SYNTH_XCD=0: plain workgroup order (A/B measurement only)
   bool identity_perm = true;
   bool has_cgain = false;
   DevBuf window, tw4, twN, twNf, twW, perm, cgain;
@@ -557,6 +558,7 @@ static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64
   a.out_limit = out_limit;
   a.ranges = p->ranges;
   a.no_reuse = p->no_reuse;
+  a.xcd = p->xcd;
   a.timing_mask = p->timing_mask;
   {
     ProfScope ps(2, (double)p->n_pol * (nb * p->keep * p->N * 8.0 + nb * p->Lkeep * 8.0), s);
@@ -627,6 +629,7 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
   if (const char* v = std::getenv("PFB_SYNTH_RANGES")) p->ranges = std::max(-1, std::atoi(v));
   if (const char* v = std::getenv("PFB_TIMING_MASK")) p->timing_mask = std::atoi(v);
   if (const char* v = std::getenv("PFB_SYNTH_NO_REUSE")) p->no_reuse = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PFB_SYNTH_XCD")) p->xcd = std::atoi(v) != 0;
   if (const char* v = std::getenv("PFB_RT_CHUNK_BLOCKS")) p->rt_chunk_blocks = std::max(1, std::atoi(v));
   p->N = N;
   p->nu = nu;

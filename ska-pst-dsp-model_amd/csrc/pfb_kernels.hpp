@@ -73,6 +73,7 @@ struct SynthBlockArgs {
   int64_t out_limit;       // samples per pol actually written (InverseFilterBank trim)
   int ranges;              // 0: one workgroup per block; -1 persistent auto; >0 persistent ranges
   int no_reuse;            // 1: re-read the 2 Ov overlap rows from HBM (PFB_SYNTH_NO_REUSE, A/B only)
+  int xcd;                 // 1: XCD-aware workgroup -> (phase group, range) order (PFB_SYNTH_XCD)
   int timing_mask;         // timing experiments only (PFB_TIMING_MASK): bit0 drop Z loads,
                            // bit1 drop output stores, bit2 drop tw4 loads (results invalid)
 };

@@ -234,8 +234,11 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
   const int tid = threadIdx.x;
   const int N = a.N;
   const int groups = N / TG;
-  const int tg = blockIdx.x % groups;
-  const int rr = blockIdx.x / groups;
+  // XCD-aware: consecutive phase groups (which share Z and output cache lines when
+  // TG * 8 B < 128 B, e.g. SKA-Mid's TG = 4) land on the same XCD and its L2
+  const int lt = a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int tg = lt % groups;
+  const int rr = lt / groups;
   const int Rg = gridDim.x / groups;
   // PERSIST: a contiguous range of blocks per workgroup.  (Strided assignment rr + k Rg
   // keeps the 2 Ov overlap rows in L2, -30 % HBM reads, but measured 10 % slower.)
