@@ -21,6 +21,7 @@
 #include <limits>
 #include <type_traits>
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <mutex>
 #include <vector>
@@ -159,14 +160,22 @@ __global__ void __launch_bounds__(TPB) transpose_kernel(const float2* __restrict
 
 // ---------------------------------------------------------------- quantisation
 // stats[0..2] += (sum re, sum im, sum |x|^2) in double over n_pol rows of n samples
+// (grid: x = grid-stride over one row, y = polarisation; 16-byte loads of two samples)
 __global__ void __launch_bounds__(TPB) moments_kernel(const float2* __restrict__ x, int64_t ps,
                                                       int64_t n, int n_pol, double* stats) {
   double sr = 0, si = 0, s2 = 0;
-  const int64_t total = n * n_pol;
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * TPB) {
-    const int64_t p = i / n, t = i - p * n;
-    const float2 v = x[p * ps + t];
+  const float2* row = x + blockIdx.y * ps;
+  const bool vec = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
+  const int64_t n2 = vec ? n / 2 : 0;
+  const int64_t stride = (int64_t)gridDim.x * TPB;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n2; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(row)[i];
+    sr += (double)v.x + (double)v.z;
+    si += (double)v.y + (double)v.w;
+    s2 += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+  }
+  for (int64_t i = 2 * n2 + (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += stride) {
+    const float2 v = row[i];
     sr += v.x;
     si += v.y;
     s2 += (double)v.x * v.x + (double)v.y * v.y;
@@ -198,7 +207,7 @@ __global__ void __launch_bounds__(TPB) moments_kernel(const float2* __restrict__
 }
 
 // y = round(single(scale) * x) (Matlab round: half away from zero), scale = rms/std or 1;
-// stats[3] receives the scale (thread 0 of block 0) for the host to read back
+// stats[3] receives the scale (thread 0 of block (0, 0)) for the host to read back
 __global__ void __launch_bounds__(TPB) quantize_kernel(const float2* __restrict__ x, int64_t ips,
                                                        float2* __restrict__ y, int64_t ops, int64_t n,
                                                        int n_pol, double rms, double* stats) {
@@ -210,13 +219,12 @@ __global__ void __launch_bounds__(TPB) quantize_kernel(const float2* __restrict_
     scale = rms / sqrt(var);
   }
   const float sf = (float)scale;  // single * double -> single (Matlab mixed-class rule)
-  if (blockIdx.x == 0 && threadIdx.x == 0) stats[3] = scale;
-  const int64_t total = n * n_pol;
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * TPB) {
-    const int64_t p = i / n, t = i - p * n;
-    const float2 v = x[p * ips + t];
-    y[p * ops + t] = make_float2(roundf(sf * v.x), roundf(sf * v.y));
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) stats[3] = scale;
+  const float2* xr = x + blockIdx.y * ips;
+  float2* yr = y + blockIdx.y * ops;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    const float2 v = xr[i];
+    yr[i] = make_float2(roundf(sf * v.x), roundf(sf * v.y));
   }
 }
 
@@ -341,7 +349,8 @@ pfb_status pfb_quantize(const pfb_cf32* in, int64_t in_pol_stride, int64_t n, in
   hipStream_t s = (hipStream_t)stream;
   double* st = nullptr;
   LCHK(stats_buffer(&st));
-  const unsigned g = grid_stride_blocks(n * n_pol);
+  if (n_pol > 65535) return bad("pfb_quantize: n_pol > 65535");
+  const dim3 g(std::max(1u, grid_stride_blocks(n * n_pol) / (unsigned)n_pol), (unsigned)n_pol);
   if (rms > 0) {
     LCHK(hipMemsetAsync(st, 0, 3 * sizeof(double), s));
     hipLaunchKernelGGL(moments_kernel, g, TPB, 0, s, (const float2*)in, in_pol_stride, n, n_pol, st);

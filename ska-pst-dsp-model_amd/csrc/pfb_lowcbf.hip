@@ -16,6 +16,7 @@
 // channel selection and scale on its way to HBM.  HBM-bound: 8 B read per input
 // sample, 216 * 8 B written per 192 input samples.
 #include "pfb_common.hpp"
+#include "pfb_pair.hpp"
 
 namespace pfb {
 
@@ -59,17 +60,41 @@ __global__ __launch_bounds__(NT) void lowcbf_kernel(LowCbfArgs a) {
   const bool interior = k0 * LM - a.pad >= 0 &&
                         (k0 + LROWS - 1) * LM + LN * LP - a.pad <= a.n_dat && k0 + LROWS <= a.K;
   if (interior) {
+    // 4 M = 3 N: row k + 4 reads the samples of row k shifted by 3 taps, so each of the
+    // 4 commutator residues keeps a 12-sample register window and loads 3 new samples
+    // per row (84 loads per thread instead of 192)
+    static_assert(4 * LM == 3 * LN && LROWS % 4 == 0, "commutator period");
     const float2* __restrict__ xb = x + (k0 * LM + n - a.pad);
-#pragma unroll 4
-    for (int r = 0; r < LROWS; ++r) {
-      float ax = 0.f, ay = 0.f;
+#pragma unroll 1
+    for (int rho = 0; rho < 4; ++rho) {
+      v2f w[LP];
 #pragma unroll
       for (int m = 0; m < LP; ++m) {
-        const float2 v = xb[r * LM + m * LN];
-        ax = fmaf(f[m], v.x, ax);
-        ay = fmaf(f[m], v.y, ay);
+        const float2 v = xb[rho * LM + m * LN];
+        w[m] = v2f{v.x, v.y};
       }
-      rows.store(r, n, make_float2(ax, ay));
+#pragma unroll
+      for (int jj = 0; jj < LROWS / 4; ++jj) {
+        const int r = rho + 4 * jj;
+        v2f nw[3];
+        if (jj + 1 < LROWS / 4) {
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const float2 v = xb[(r + 4) * LM + (LP - 3 + i) * LN];
+            nw[i] = v2f{v.x, v.y};
+          }
+        }
+        v2f acc{0.f, 0.f};
+#pragma unroll
+        for (int m = 0; m < LP; ++m) acc = __builtin_elementwise_fma(v2f{f[m], f[m]}, w[m], acc);
+        rows.store(r, n, make_float2(acc.x, acc.y));
+        if (jj + 1 < LROWS / 4) {
+#pragma unroll
+          for (int m = 0; m < LP - 3; ++m) w[m] = w[m + 3];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) w[LP - 3 + i] = nw[i];
+        }
+      }
     }
   } else {
     for (int r = 0; r < LROWS; ++r) {

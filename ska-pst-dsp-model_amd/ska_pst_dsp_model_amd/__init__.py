@@ -17,7 +17,7 @@ from .filterbank import (Channelizer, DeChannelizer, FilterBank, InverseFilterBa
 from .firio import (design_PFB_FIR_filter, design_PFB_FIR_filter_two_stage,
                     read_fir_filter_coeff)
 from .window import PFBWindow, identity_taper
-from . import dada, harness, layout, sharding
+from . import dada, harness, layout, sharding, verify
 
 __all__ = [
     "PfbError", "device_count", "Rational", "default_config", "load_config", "AnalysisPlan",

@@ -89,3 +89,16 @@ def test_harness_names():
     assert harness._num2str(241.92) == "241.92"
     assert harness._num2str(2.0) == "2"
     assert harness._num2str(1.0 / 7) == "0.14286"
+
+
+def test_verify_metrics_match_util_definitions():
+    from ska_pst_dsp_model_amd import verify
+    a = np.array([1.0, 0.1, 0.01, 3.0])
+    assert np.array_equal(verify.spurious(a), [1.0, 0.1, 0.01, 0.0])
+    p = np.abs(a) ** 2
+    assert np.isclose(verify.total_spurious(a), 10 * np.log10(1 + 0.01 + 1e-4 + 1e-13))
+    assert np.isclose(verify.max_spurious(a), 10 * np.log10(1 + 1e-13))
+    assert np.isclose(verify.mean_spurious(a), 10 * np.log10((p.sum() - 9) / 4 + 1e-13))
+    al = verify.purity_alignment(8, "8/7", 128, 16, 81, 3)
+    assert al == {"normalize": 1024, "block_size": 896, "fft_size": 1792, "n_samples": 2688,
+                  "output_sample_shift": 112, "total_sample_shift": 152}

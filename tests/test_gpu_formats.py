@@ -304,3 +304,50 @@ def test_lowcbf_filterbank_stream(gpu):
         assert got.shape == ref.shape, (got.shape, ref.shape)
         assert_pfb_close(got, ref, what=f"lowcbf stream n={n}")
         assert fb.buffered_samples == ofb.buffered_samples
+
+
+# ----------------------------------------------------------------------------- purity
+def test_purity_impulse_and_tone_through_dada_pipeline(gpu, tmp_path):
+    """The reference's fidelity requirements scored with verify.py on the hip backend,
+    end to end through DADA files: a temporal impulse (TestImpulse.m:46-73, <= -60 dB
+    outside +-1 sample) and a pure tone (TestPureTone.m:55-89, <= -60 dB spurious),
+    SKA-Low 256 channels 4/3 (config 'low')."""
+    pfb = _pfb()
+    from ska_pst_dsp_model_amd import harness, verify
+    taps = pfb.design_PFB_FIR_filter(256, "4/3", 12)
+    fir = tmp_path / "low.txt"
+    np.savetxt(fir, taps[None, :])
+    al = verify.purity_alignment(256, "4/3", 256, 48, len(taps), 3)
+    n = 1 << 18
+    off = 100000
+    run = harness.pipeline(
+        harness.partial(harness.generate_test_vector, domain_name="time", n_bins=n),
+        harness.partial(harness.channelize, channels=256, os_factor_str="4/3",
+                        fir_filter_path=str(fir)),
+        harness.partial(harness.synthesize, input_fft_length=256, input_overlap=48,
+                        fft_window_str="tukey"),
+        output_dir=str(tmp_path))
+    _, _, sy = run([off], [1])
+    y = sy.data[:, 0, 0]
+    # the header taps are '%0.6E'-rounded; the delay is (L_h - 1)/2 + output overlap
+    pos = off - al["total_sample_shift"]
+    assert abs(int(np.argmax(np.abs(y))) - pos) <= 1
+    amp = 20 * np.log10(np.abs(y) / np.abs(y).max() + 1e-30)
+    mask = np.ones(len(y), bool)
+    mask[pos - 1:pos + 2] = False
+    assert amp[mask].max() <= -60.0, amp[mask].max()
+    # pure tone, an integral number of periods in the scored span
+    run2 = harness.pipeline(
+        harness.partial(harness.generate_test_vector, domain_name="freq", n_bins=n),
+        harness.partial(harness.channelize, channels=256, os_factor_str="4/3",
+                        fir_filter_path=str(fir)),
+        harness.partial(harness.synthesize, input_fft_length=256, input_overlap=48,
+                        fft_window_str="tukey"),
+        output_dir=str(tmp_path / "tone"))
+    (tmp_path / "tone").mkdir(exist_ok=True)
+    _, _, sy2 = run2([16], [np.pi / 4])
+    y2 = sy2.data[:, 0, 0]
+    # 16 cycles per 2^18 samples: period 16384, score an integral number of periods
+    span = (len(y2) // 16384) * 16384
+    score = verify.tone_purity(y2[:span])
+    assert score["max_spurious"] <= -60.0, score
