@@ -100,13 +100,21 @@ struct PairOut {
   __amdgpu_buffer_rsrc_t o, o1;
   int N, t1_lo, t0;
   float scale;
+  bool whole;  // the kept range ends on a pair boundary: one 16-byte store per pair
   template <class P, class RR>
   __device__ __forceinline__ void store(int q, int t1, cpx2 v, P, RR) const {
     // negative offsets (t1 < t1_lo) wrap past 2^31 bytes and are dropped by the range check
     const int off = ((t1 - t1_lo) * N + t0 + 2 * q) * 8;
     const Interleaved y = to_interleaved(cscale(v, scale));
-    __builtin_amdgcn_raw_buffer_store_b64(as_u(y.lo), o, off, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b64(as_u(y.hi), o1, off, 0, 0);
+    if (whole) {
+      // (t0 + 2q even, nk even): a pair never straddles the range end, so the 16-byte
+      // store is dropped or kept as a whole exactly when its two samples are
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(v4u, v4f{y.lo.x, y.lo.y, y.hi.x, y.hi.y}), o, off, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b64(as_u(y.lo), o, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(as_u(y.hi), o1, off, 0, 0);
+    }
   }
 };
 
@@ -270,7 +278,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
         (a.timing_mask & 2) ? 0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
     return PairOut{make_rsrc(opol + ob, (uint32_t)nk * 8u),
                    make_rsrc(opol + ob + 1, (uint32_t)max((int64_t)0, nk - 1) * 8u), N, a.t1_lo, t0,
-                   a.scale};
+                   a.scale, (nk & 1) == 0};
   };
 
   if constexpr (!SP::fused) {
