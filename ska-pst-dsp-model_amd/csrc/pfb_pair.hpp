@@ -93,6 +93,9 @@ struct LdsPairs {
   }
 };
 
+// Pair-row index that sends an HBM store out of its buffer descriptor's range (dropped).
+constexpr int kDropPair = -(1 << 24);
+
 // One Stockham pass of radix R over PAIRS pair-rows (2 * PAIRS transforms of length N).
 // Thread b owns butterfly j = b / PAIRS of pair row q = b % PAIRS (pair rows fastest).
 template <int N, int R, int NS, int DIR, int PAIRS, int NTH, class In, class Out>
@@ -101,18 +104,24 @@ __device__ __forceinline__ void stockham_pass_pair(const In& in, const Out& out,
   constexpr int NB = N / R;
   constexpr int TOT = PAIRS * NB;
   constexpr int PER = (TOT + NTH - 1) / NTH;
+  // A pass that stores to HBM with idle threads (TOT not a multiple of NTH) runs them on a
+  // clamped butterfly with their stores pointed out of range instead of branching around
+  // them: the wave then issues the same number of stores on every path, so the vmcnt
+  // bookkeeping stays exact and a later wait for a load never waits for these stores.
+  constexpr bool CLAMP = !Out::kIsLds && (TOT % NTH != 0);
   cpx2 v[PER][R];
   static_for<0, PER>([&](auto p) {
-    const int b = tid + p * NTH;
-    if (TOT % NTH == 0 || b < TOT) {
+    const int b = CLAMP ? min(tid + p * NTH, TOT - 1) : tid + p * NTH;
+    if (CLAMP || TOT % NTH == 0 || b < TOT) {
       const int q = b % PAIRS, j = b / PAIRS;
       static_for<0, R>([&](auto r) { v[p][r] = in.load(q, j + r * NB, p, r); });
     }
   });
   if constexpr (In::kIsLds && Out::kIsLds) __syncthreads();
   static_for<0, PER>([&](auto p) {
-    const int b = tid + p * NTH;
-    if (TOT % NTH == 0 || b < TOT) {
+    const int b0 = tid + p * NTH;
+    const int b = CLAMP ? min(b0, TOT - 1) : b0;
+    if (CLAMP || TOT % NTH == 0 || b < TOT) {
       const int q = b % PAIRS, j = b / PAIRS;
       const int k = j % NS;
       if constexpr (NS > 1) {
@@ -122,7 +131,8 @@ __device__ __forceinline__ void stockham_pass_pair(const In& in, const Out& out,
       }
       sdft<R, DIR>(v[p]);
       const int idxD = (j / NS) * NS * R + k;
-      static_for<0, R>([&](auto r) { out.store(q, idxD + r * NS, v[p][r], p, r); });
+      const int qs = (CLAMP && b0 >= TOT) ? kDropPair : q;
+      static_for<0, R>([&](auto r) { out.store(qs, idxD + r * NS, v[p][r], p, r); });
     }
   });
 }

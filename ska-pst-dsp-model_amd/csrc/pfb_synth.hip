@@ -91,6 +91,10 @@ struct PairSelect {
   }
 };
 
+// P16: the kept range of every block ends on a pair boundary (even output limit), so
+// one 16-byte store per sample pair is dropped or kept as a whole exactly when its two
+// samples are (t0 + 2q and Lkeep are even); otherwise two range-checked 8-byte stores.
+template <bool P16>
 struct PairOut {
   static constexpr bool kIsLds = false;
   // o: first kept output sample of the block, records = kept samples in bytes;
@@ -100,13 +104,13 @@ struct PairOut {
   __amdgpu_buffer_rsrc_t o, o1;
   int N, t1_lo, t0;
   float scale;
-  bool whole;  // the kept range ends on a pair boundary: one 16-byte store per pair
   template <class P, class RR>
   __device__ __forceinline__ void store(int q, int t1, cpx2 v, P, RR) const {
-    // negative offsets (t1 < t1_lo) wrap past 2^31 bytes and are dropped by the range check
+    // negative offsets (t1 < t1_lo, q = kDropPair) wrap past 2^31 bytes and are dropped
+    // by the range check
     const int off = ((t1 - t1_lo) * N + t0 + 2 * q) * 8;
     const Interleaved y = to_interleaved(cscale(v, scale));
-    if (whole) {
+    if constexpr (P16) {
       // (t0 + 2q even, nk even): a pair never straddles the range end, so the 16-byte
       // store is dropped or kept as a whole exactly when its two samples are
       __builtin_amdgcn_raw_buffer_store_b128(
@@ -231,7 +235,7 @@ __device__ __forceinline__ void fused_select_pass(const LdsPairs& rowsF, const L
 // first-pass register r of a thread holds row j + r NF/R1 — so the next block's
 // registers 0 .. R1-DK-1 are this block's registers DK .. R1-1: they move in registers
 // and only DK of the R1 rows are read from HBM (the 2 Ov overlap re-read disappears).
-template <int NF, int W, int PAIRS, bool SPANS, bool PERSIST, int DK = 0>
+template <int NF, int W, int PAIRS, bool SPANS, bool PERSIST, int DK = 0, bool P16 = false>
 __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void synth_block_kernel(SynthBlockArgs a) {
   using SS = SynthPairShape<NF, W, PAIRS>;
   using SP = SynthPlan<NF, W>;
@@ -276,9 +280,9 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
     const int64_t avail = a.out_limit - ob;
     const int64_t nk =
         (a.timing_mask & 2) ? 0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
-    return PairOut{make_rsrc(opol + ob, (uint32_t)nk * 8u),
+    return PairOut<P16>{make_rsrc(opol + ob, (uint32_t)nk * 8u),
                    make_rsrc(opol + ob + 1, (uint32_t)max((int64_t)0, nk - 1) * 8u), N, a.t1_lo, t0,
-                   a.scale, (nk & 1) == 0};
+                   a.scale};
   };
 
   if constexpr (!SP::fused) {
@@ -359,9 +363,13 @@ static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
     // the overlap-reuse instance when keep matches the compiled DK
     constexpr int NB1 = NF / synth_first_radix<NF, W>();
     constexpr int DK = synth_reuse_dk<NF, W>();
-    auto kern = (DK > 0 && a.keep == DK * NB1 && !a.no_reuse)
-                    ? synth_block_kernel<NF, W, PAIRS, SPANS, SynthPlan<NF, W>::fused, DK>
-                    : synth_block_kernel<NF, W, PAIRS, SPANS, SynthPlan<NF, W>::fused, 0>;
+    constexpr bool FU = SynthPlan<NF, W>::fused;
+    const bool reuse = DK > 0 && a.keep == DK * NB1 && !a.no_reuse;
+    const bool p16 = (a.out_limit % 2 == 0) && (a.Lkeep % 2 == 0);
+    auto kern = reuse ? (p16 ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true>
+                             : synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, false>)
+                      : (p16 ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, 0, true>
+                             : synth_block_kernel<NF, W, PAIRS, SPANS, FU, 0, false>);
     hipError_t e = set_lds(kern, SS::lds_bytes);
     if (e != hipSuccess) return e;
     const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / SS::lds_bytes));
