@@ -448,8 +448,7 @@ static hipError_t launch_fused(const AnalysisArgs& a, hipStream_t s) {
   hipError_t e = set_lds(kern, bytes);
   if (e != hipSuccess) return e;
   dim3 grid((unsigned)((a.K - a.row0 + S_::T - 1) / S_::T), (unsigned)a.n_pol);
-  hipLaunchKernelGGL(kern, grid, dim3(NT), bytes, s, a);
-  return hipGetLastError();
+  return launch_kernel(kern, grid, dim3(NT), bytes, s, a);
 }
 
 template <int N, int P, int NU, int DE>
@@ -465,8 +464,7 @@ static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
   const int64_t per_pol = std::max<int64_t>(1, (per_cu * cu_count()) / a.n_pol);
   const int64_t wgs = std::min<int64_t>(n_steps, per_pol);
   dim3 grid((unsigned)wgs, (unsigned)a.n_pol);
-  hipLaunchKernelGGL(kern, grid, dim3(NT), SH::lds_bytes, s, a);
-  return hipGetLastError();
+  return launch_kernel(kern, grid, dim3(NT), SH::lds_bytes, s, a);
 }
 
 // streaming kernel for the SKA-Low shapes (N = 256, Bunton); 0 = not compiled

@@ -118,22 +118,41 @@ struct Profiler {
   }
 };
 Profiler g_prof;
+thread_local pfb::LaunchEvents g_armed;
 
+// Times the launch(es) issued while in scope.  single = true: exactly one kernel launch
+// goes through pfb::launch_kernel, which records the two events inside its own dispatch
+// (hipExtLaunchKernelGGL) — the kernel's own duration, as a kernel trace measures it.
+// single = false (multi-kernel paths): events recorded on the stream around the scope.
 struct ProfScope {
   hipEvent_t a = nullptr, b = nullptr;
   int which;
   double bytes;
   hipStream_t s;
-  ProfScope(int w, double by, hipStream_t st) : which(w), bytes(by), s(st) {
+  bool single;
+  ProfScope(int w, double by, hipStream_t st, bool one = true) : which(w), bytes(by), s(st), single(one) {
     if (g_prof.enabled) {
       a = g_prof.get();
       b = g_prof.get();
-      if (a) (void)hipEventRecord(a, s);
+      if (a && b) {
+        if (single) pfb::armed_launch_events() = pfb::LaunchEvents{a, b};
+        else (void)hipEventRecord(a, s);
+      }
     }
   }
   ~ProfScope() {
     if (g_prof.enabled && a && b) {
-      (void)hipEventRecord(b, s);
+      if (single) {
+        pfb::LaunchEvents& ev = pfb::armed_launch_events();
+        if (ev.start) {  // not consumed (no kernel launched): drop the record
+          ev = pfb::LaunchEvents{};
+          g_prof.pool.push_back(a);
+          g_prof.pool.push_back(b);
+          return;
+        }
+      } else {
+        (void)hipEventRecord(b, s);
+      }
       g_prof.pending.push_back({which, a, b, bytes});
     }
   }
@@ -152,6 +171,8 @@ hipError_t copy_pols(float2* dst, int64_t dps, const float2* src, int64_t sps, i
 }
 
 }  // namespace
+
+pfb::LaunchEvents& pfb::armed_launch_events() { return g_armed; }
 
 // error channel shared with the other C-ABI translation units (pfb_layout.hip)
 pfb_status pfb_set_error(pfb_status s, const char* msg) { return fail(s, "%s", msg); }
@@ -240,7 +261,7 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   // (with z: the stage-1 rows are a synthesis intermediate, not algorithmic bytes —
   // the synthesis' algorithmic read of its input is counted by the block kernel)
   const double bytes = (double)p->n_pol * (8.0 * in_samples + 8.0 * (K_end - row0) * p->N);
-  ProfScope ps(z ? 3 : 0, bytes, s);
+  ProfScope ps(z ? 3 : 0, bytes, s, p->fused);  // generic path = FIR + row FFT launches
   HIPCHK(pfb::launch_analysis(a, s));
   return PFB_OK;
 }

@@ -3,6 +3,8 @@
 // tile order, the row-FFT kernel template and launch helpers.
 #pragma once
 
+#include <hip/hip_ext.h>
+
 #include "pfb_device.hpp"
 #include "pfb_kernels.hpp"
 #include "pfb_pair.hpp"
@@ -173,6 +175,19 @@ __global__ __launch_bounds__(NT) void row_fft_kernel(RowFftArgs a) {
 
 
 // ======================================================================= launchers
+// Launch through hipExtLaunchKernelGGL when the profiler has armed events (they are
+// consumed by this launch), else a plain launch.
+template <class K, class... Args>
+inline hipError_t launch_kernel(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t s, Args... args) {
+  LaunchEvents& ev = armed_launch_events();
+  if (ev.start && ev.stop) {
+    hipExtLaunchKernelGGL(kern, grid, block, (uint32_t)lds, s, ev.start, ev.stop, 0, args...);
+    ev = LaunchEvents{};
+  } else {
+    hipLaunchKernelGGL(kern, grid, block, lds, s, args...);
+  }
+  return hipGetLastError();
+}
 template <class K>
 inline hipError_t set_lds(K kernel, size_t bytes) {
   if (bytes > 65536) {

@@ -95,6 +95,14 @@ struct LowCbfArgs {
 };
 hipError_t launch_lowcbf(const LowCbfArgs& a, hipStream_t s);
 
+// Kernel timing (pfb_profile_*): when the C-ABI profiler arms these events, the next
+// single-kernel launch records them in its own dispatch (hipExtLaunchKernelGGL), so the
+// measured interval is the kernel alone, as a kernel trace sees it.
+struct LaunchEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchEvents& armed_launch_events();
+
 bool analysis_supported(int N, int P, int variant, bool* fused);
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s);
 bool chan_ifft_supported(int N);

@@ -128,8 +128,7 @@ hipError_t launch_lowcbf(const LowCbfArgs& a, hipStream_t s) {
   hipError_t e = set_lds(lowcbf_kernel, bytes);
   if (e != hipSuccess) return e;
   dim3 grid((unsigned)((a.K + LROWS - 1) / LROWS), (unsigned)a.n_pol);
-  hipLaunchKernelGGL(lowcbf_kernel, grid, dim3(NT), bytes, s, a);
-  return hipGetLastError();
+  return launch_kernel(lowcbf_kernel, grid, dim3(NT), bytes, s, a);
 }
 
 }  // namespace pfb

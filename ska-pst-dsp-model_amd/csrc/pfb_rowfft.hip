@@ -13,8 +13,7 @@ static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s
   hipError_t e = set_lds(kern, bytes);
   if (e != hipSuccess) return e;
   dim3 grid((unsigned)((r.n_rows + ROWS - 1) / ROWS), (unsigned)n_pol);
-  hipLaunchKernelGGL(kern, grid, dim3(NT), bytes, s, r);
-  return hipGetLastError();
+  return launch_kernel(kern, grid, dim3(NT), bytes, s, r);
 }
 
 template <int N, int DIR>

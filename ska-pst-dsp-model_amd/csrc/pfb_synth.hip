@@ -376,15 +376,13 @@ static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
     int ranges = a.ranges > 0 ? a.ranges : std::max(1, cu_count() * per_cu / (groups * a.n_pol));
     ranges = std::min(ranges, a.n_blocks);
     dim3 grid((unsigned)(groups * ranges), (unsigned)a.n_pol);
-    hipLaunchKernelGGL(kern, grid, dim3(NTP), SS::lds_bytes, s, a);
-    return hipGetLastError();
+    return launch_kernel(kern, grid, dim3(NTP), SS::lds_bytes, s, a);
   }
   auto kern = synth_block_kernel<NF, W, PAIRS, SPANS, false>;
   hipError_t e = set_lds(kern, SS::lds_bytes);
   if (e != hipSuccess) return e;
   dim3 grid((unsigned)(groups * a.n_blocks), (unsigned)a.n_pol);
-  hipLaunchKernelGGL(kern, grid, dim3(NTP), SS::lds_bytes, s, a);
-  return hipGetLastError();
+  return launch_kernel(kern, grid, dim3(NTP), SS::lds_bytes, s, a);
 }
 
 // pair rows per workgroup: enough for every thread to own one first-pass butterfly,
