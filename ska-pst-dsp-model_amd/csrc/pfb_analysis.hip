@@ -259,26 +259,25 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
         });
       });
     });
+    const int64_t k0 = (q_lo + stp * QS) * NU;
+    // ZOUT: the synthesis stage-1 row of output row k is the N-point inverse DFT across
+    // channels of out[k] = N FFT_N(v_k), i.e. N^2 v_k exactly — the FIR output this
+    // thread already holds at position c (v_k[c]).  It goes to HBM straight from the
+    // registers (no inverse FFT; N^2 is a power of two, so the scaling is exact).
+    const BufRowStore zs = BufRowStore::rows(ZOUT ? zpol : opol, k0, T, max(a.row0, a.z_row0), a.K,
+                                             N, (float)N * (float)N);
     static_for<0, NU>([&](auto sv) {
       constexpr int s = decltype(sv)::value;
       static_for<0, QS>([&](auto qv) {
         constexpr int qq = decltype(qv)::value;
-        rows.store(qq * NU + s, c, make_float2(acc[s][qq].x, acc[s][qq].y));
+        const float2 v = make_float2(acc[s][qq].x, acc[s][qq].y);
+        rows.store(qq * NU + s, c, v);
+        if constexpr (ZOUT) zs.store(qq * NU + s, c, v);
       });
     });
     __syncthreads();
-    const int64_t k0 = (q_lo + stp * QS) * NU;
     const BufRowStore st = BufRowStore::rows(opol, k0, T, a.row0, a.K, N, (float)N);
-    if constexpr (ZOUT) {
-      // analysis FFT -> HBM + LDS; then the synthesis channel IFFT -> Z (row_fft_kernel
-      // <N, +1>'s passes on the same values)
-      block_fft<N, -1, T, NT>(rows, BufStoreKeep{st, rows}, rows, tw, c);
-      __syncthreads();
-      const BufRowStore zs = BufRowStore::rows(zpol, k0, T, max(a.row0, a.z_row0), a.K, N, 1.0f);
-      block_fft<N, +1, T, NT>(rows, zs, rows, tw, c);
-    } else {
-      block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
-    }
+    block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
 #pragma unroll
     for (int i = 0; i < PE - 1; ++i) win[i] = win[i + NEW];
 #pragma unroll

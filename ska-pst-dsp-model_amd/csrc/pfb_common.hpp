@@ -61,19 +61,6 @@ struct BufRowStore {
   }
 };
 
-// The analysis FFT's last pass in the round trip, branch-free (BufRowStore): the row
-// goes to HBM and back into the LDS rows for the synthesis channel IFFT.
-struct BufStoreKeep {
-  static constexpr bool kIsLds = true;
-  BufRowStore hbm;
-  LdsIO lds;
-  __device__ __forceinline__ void store(int row, int c, float2 v) const {
-    const float2 y = cscale(v, hbm.scale);
-    const uint32_t off = row >= hbm.lo ? (uint32_t)((row * hbm.N + c) * 8) : 0xFFFFFFF0u;
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y), hbm.r, off, 0, 0);
-    lds.store(row, c, y);
-  }
-};
 
 // Row loader of the first FFT pass.  Rows past the end are clamped to the last valid
 // row (their results are never stored), so every load is unconditional and the

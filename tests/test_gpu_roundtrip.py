@@ -1,8 +1,14 @@
 """GPU tests of the pipelined round trip (pfb_roundtrip_execute) and full-size parity.
 
-* The pipelined analysis -> synthesis must be bit-identical to the two separate calls
-  (same kernels, same inputs per row and per block; only the launch order differs) —
-  for both analysis variants, several chunk sizes, sample offsets and polarisations.
+* The channelised product of the round trip is bit-identical to the separate analysis
+  call.  The synthesised output is bit-identical to the separate synthesis call on the
+  chunked pipeline (same kernels, same inputs per block; only the launch order
+  differs).  On the fused path (chunk 0 with the streaming analysis shapes) the
+  synthesis stage-1 rows are N^2 v_k taken before the analysis FFT instead of the
+  channel IFFT of the rounded channelised row — the same quantity in exact arithmetic —
+  so there the output agrees with the separate calls to the reference's 1e-6
+  (relative to the peak), for both analysis variants, several chunk sizes, sample
+  offsets and polarisations.
 * At the BASELINE C2 size (2^24 samples, 256 ch, OS 8/7, 3073 taps, Nf 256, Ov 48,
   tukey, deripple) the round trip is compared with the float64 oracle at the
   reference's 1e-6 criterion (test_matlab_dspsr_pfb_inversion.py:35,151-152), and a
@@ -47,7 +53,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_roundtrip_bit_identical_to_separate_calls(gpu, case):
+def test_roundtrip_matches_separate_calls(gpu, case):
     import torch
     pfb = _pfb()
     N, os_, tpc, nf, ov, variant, n_pol, n_dat, cb, so = case
@@ -65,7 +71,11 @@ def test_roundtrip_bit_identical_to_separate_calls(gpu, case):
     assert chan.shape == chan_ref.shape and out.shape == out_ref.shape
     assert out.shape[1] > 0
     assert torch.equal(chan, chan_ref), "channelised product differs"
-    assert torch.equal(out, out_ref), "synthesised output differs"
+    fused = (cb == 0 and N == 256 and variant == "polyphase_analysis" and tpc in (11, 12))
+    if fused:
+        assert_pfb_close(out.cpu().numpy(), out_ref.cpu().numpy(), what="fused round trip")
+    else:
+        assert torch.equal(out, out_ref), "synthesised output differs"
 
 
 def test_roundtrip_no_blocks_only_analysis(gpu):
@@ -107,13 +117,13 @@ def test_roundtrip_graph_capture(gpu, chunk_blocks):
     ana = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
     win = pfb.PFBWindow().lookup["tukey"](256, 48)
     syn = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, 1, 0)
-    chan_ref = ana.execute(x)
-    out_ref = syn.execute(chan_ref, layout="ptc")
     if chunk_blocks:
         syn.set_chunk_blocks(chunk_blocks)
+    chan_ref, out_ref = pfb.roundtrip(ana, syn, x)  # eager reference (also the warm-up)
+    chan_ref, out_ref = chan_ref.clone(), out_ref.clone()
     chan = torch.empty_like(chan_ref)
     out = torch.empty_like(out_ref)
-    pfb.roundtrip(ana, syn, x, chan=chan, out=out)  # warm-up (allocates plan buffers)
+    pfb.roundtrip(ana, syn, x, chan=chan, out=out)
     torch.cuda.synchronize()
     chan.zero_()
     out.zero_()
