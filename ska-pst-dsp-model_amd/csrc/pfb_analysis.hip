@@ -373,6 +373,13 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
     pos = (n - ix + N) % N;
   }
   float2* sc = a.scratch + (int64_t)pol * (a.K - a.row0) * N + pos;
+  // round trip (a.z): the synthesis stage-1 row of channelised row t is the N-point
+  // inverse DFT across channels of row t = the row FFT of these sums, i.e. N^2 times
+  // this row (Bunton: same column; padded, whose row FFT is an inverse one: column
+  // (-pos) mod N), at the padded variant's circularly shifted row t = (k - sds) mod K
+  float2* zc = a.z ? a.z + pol * a.z_pol_stride + (VARIANT == kBunton ? pos : (N - pos) % N)
+                   : nullptr;
+  const float zscale = (float)N * (float)N;
 #pragma unroll 1
   for (int64_t j = j0; j < j1; ++j) {
     const int64_t k = s + (int64_t)NU * j;
@@ -389,6 +396,14 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
     }
     const v2f acc = acc0 + acc1;
     sc[(k - a.row0) * N] = make_float2(acc.x, acc.y);
+    if (zc) {
+      int64_t t = k;
+      if constexpr (VARIANT != kBunton) {
+        t = k - a.sds;
+        while (t < 0) t += a.K_total;
+      }
+      if (t >= a.z_row0) zc[(t - a.z_row0) * N] = make_float2(zscale * acc.x, zscale * acc.y);
+    }
     if constexpr (VARIANT == kBunton) {
 #pragma unroll
       for (int p = 0; p < PW - DE; ++p) w[p] = w[p + DE];
@@ -427,9 +442,15 @@ static bool launch_fir_window_de(const AnalysisArgs& a, hipStream_t s, hipError_
   return true;
 }
 
-static bool launch_fir_window(const AnalysisArgs& a, hipStream_t s, hipError_t* e) {
+static bool fir_window_applies(const AnalysisArgs& a) {
   if (a.N % NT != 0 || (int64_t)a.M * a.nu % a.N != 0) return false;
   if (std::getenv("PFB_FIR_NO_WINDOW")) return false;
+  const int de = (int)((int64_t)a.M * a.nu / a.N);
+  return (de == 7 || de == 3 || de == 27) && a.P <= 32 && a.P >= de;
+}
+
+static bool launch_fir_window(const AnalysisArgs& a, hipStream_t s, hipError_t* e) {
+  if (!fir_window_applies(a)) return false;
   const int de = (int)((int64_t)a.M * a.nu / a.N);
   if (de == 7) return launch_fir_window_de<7>(a, s, e);
   if (de == 3) return launch_fir_window_de<3>(a, s, e);
@@ -504,7 +525,9 @@ bool analysis_supported(int N, int P, int variant, bool* fused) {
 }
 
 bool analysis_can_emit_z(const AnalysisArgs& a) {
-  return stream_shape(a) && std::getenv("PFB_ANALYSIS_NO_STREAM") == nullptr;
+  if (stream_shape(a) && std::getenv("PFB_ANALYSIS_NO_STREAM") == nullptr) return true;
+  bool fused = false;
+  return analysis_supported(a.N, a.P, a.variant, &fused) && !fused && fir_window_applies(a);
 }
 
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {

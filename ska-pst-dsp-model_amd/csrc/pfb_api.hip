@@ -273,7 +273,7 @@ static bool analysis_emits_z(const pfb_analysis_plan* p) {
   a.M = p->M;
   a.P = p->P;
   a.nu = p->nu;
-  return p->fused && pfb::analysis_can_emit_z(a);
+  return pfb::analysis_can_emit_z(a);  // streaming kernel (N = 256) or register-window FIR
 }
 
 static int64_t analysis_K(const pfb_analysis_plan* p, int64_t n_dat) {

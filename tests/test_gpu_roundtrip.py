@@ -47,6 +47,11 @@ CASES = [
     # emits the synthesis stage-1 rows)
     (256, "4/3", 12, 256, 48, "polyphase_analysis", 2, 1 << 19, 0, 3),
     (256, "8/7", 11, 256, 48, "polyphase_analysis", 1, (1 << 19) + 777, 0, 2),
+    # N > 256: the register-window FIR emits the stage-1 rows (fused with chunk 0)
+    (512, "8/7", 12, 128, 16, "polyphase_analysis", 2, 1 << 19, 0, 1),
+    (512, "8/7", 12, 128, 16, "polyphase_analysis_padded", 1, 1 << 19, 0, 4),
+    (1024, "4/3", 12, 256, 48, "polyphase_analysis_padded", 2, 1 << 19, 0, 1),
+    (512, "8/7", 12, 128, 16, "polyphase_analysis_padded", 1, 1 << 19, 3, 1),
     (8, "8/7", 10, 128, 16, "polyphase_analysis", 2, 9000, 1, 1),
     (8, "8/7", 10, 128, 16, "polyphase_analysis_padded", 1, 9000, 2, 3),
 ]
@@ -71,7 +76,8 @@ def test_roundtrip_matches_separate_calls(gpu, case):
     assert chan.shape == chan_ref.shape and out.shape == out_ref.shape
     assert out.shape[1] > 0
     assert torch.equal(chan, chan_ref), "channelised product differs"
-    fused = (cb == 0 and N == 256 and variant == "polyphase_analysis" and tpc in (11, 12))
+    fused = cb == 0 and ((N == 256 and variant == "polyphase_analysis" and tpc in (11, 12))
+                         or N > 256)
     if fused:
         assert_pfb_close(out.cpu().numpy(), out_ref.cpu().numpy(), what="fused round trip")
     else:
