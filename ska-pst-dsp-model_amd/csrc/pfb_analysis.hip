@@ -395,7 +395,7 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
       if (p + 1 < PW) acc1 = __builtin_elementwise_fma(v2f{f[p + 1], f[p + 1]}, w[p + 1], acc1);
     }
     const v2f acc = acc0 + acc1;
-    sc[(k - a.row0) * N] = make_float2(acc.x, acc.y);
+    if (!zc) sc[(k - a.row0) * N] = make_float2(acc.x, acc.y);
     if (zc) {
       int64_t t = k;
       if constexpr (VARIANT != kBunton) {
@@ -553,7 +553,7 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
       default: return hipErrorInvalidValue;
     }
   }
-  if (!a.scratch) return hipErrorInvalidValue;
+  if (!a.scratch && !a.z) return hipErrorInvalidValue;
   // generic: FIR into scratch, then row FFT (with the padded circular time shift)
   const int64_t rows = a.K - a.row0;
   const int64_t total = rows * a.N;
@@ -565,6 +565,16 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
     e = hipGetLastError();
   }
   if (e != hipSuccess) return e;
+  if (a.z) {
+    // round trip: the channelised rows come from the Z rows (already in output-row order,
+    // N^2 x the FIR sums, index-reversed for the padded variant): the same row FFT on
+    // the same values scaled by 2^k, so the result is bit-identical to the scratch path
+    if (a.row0 != 0 || a.z_row0 != 0 || (a.variant == kPadded && !a.zrev)) return hipErrorInvalidValue;
+    RowFftArgs rz{a.z, a.z_pol_stride, a.out, a.out_pol_stride, rows, a.zrev, nullptr, a.twN,
+                  1.0f / (float)a.N, 0, 0, 0, a.K_total};
+    if (a.variant == kBunton) return dispatch_row_fft<-1>(a.N, rz, a.n_pol, s);
+    return dispatch_row_fft<+1>(a.N, rz, a.n_pol, s);
+  }
   RowFftArgs r{a.scratch, rows * a.N, a.out, a.out_pol_stride, rows, nullptr, nullptr, a.twN,
                (float)a.N, a.sds, a.variant == kPadded, a.row0, a.K_total};
   if (a.variant == kBunton) return dispatch_row_fft<-1>(a.N, r, a.n_pol, s);

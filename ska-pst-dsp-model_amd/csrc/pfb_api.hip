@@ -192,6 +192,7 @@ struct pfb_analysis_plan {
   int64_t n_taps = 0;
   bool fused = false;
   DevBuf taps, twN, scratch;
+  DevBuf zrev;  // padded generic round trip: index reversal (N - i) mod N of the row FFT input
   // streaming (FilterBank.m:13-14 input_buffer / buffered_samples)
   DevBuf carry, work, stage_in, stage_out;
   int64_t buffered = 0;
@@ -248,8 +249,9 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   a.variant = p->variant;
   a.taps = p->taps.as<float>();
   a.twN = p->twN.as<float2>();
+  a.zrev = p->zrev.p ? p->zrev.as<int>() : nullptr;
   a.scratch = nullptr;
-  if (!p->fused) {
+  if (!p->fused && !z) {
     HIPCHK(p->scratch.ensure((size_t)p->n_pol * (K_end - row0) * p->N * sizeof(float2)));
     a.scratch = p->scratch.as<float2>();
   }
@@ -354,6 +356,11 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
   for (int64_t i = 0; i < d->n_taps; ++i) taps[(size_t)i] = (float)d->taps[i];  // cast(filt, 'single')
   hipError_t e = upload(p->taps, taps);
   if (e == hipSuccess) e = upload(p->twN, twiddles(p->N, -1));
+  if (e == hipSuccess && !p->fused && p->variant == pfb::kPadded) {
+    std::vector<int> rev((size_t)p->N);
+    for (int i = 0; i < p->N; ++i) rev[(size_t)i] = (p->N - i) % p->N;
+    e = upload(p->zrev, rev);
+  }
   if (e != hipSuccess) {
     delete p;
     return fail(PFB_ERR_HIP, "analysis plan upload: %s", hipGetErrorString(e));
@@ -367,6 +374,7 @@ pfb_status pfb_analysis_plan_destroy(pfb_analysis_plan* p) {
   (void)hipSetDevice(p->device);
   p->taps.release();
   p->twN.release();
+  p->zrev.release();
   p->scratch.release();
   p->carry.release();
   p->work.release();
@@ -971,11 +979,16 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
   const size_t zbytes = (size_t)pa->n_pol * zrows * pa->N * sizeof(float2);
   if (!no_fuse && analysis_emits_z(pa) && ps->identity_perm && !ps->has_cgain &&
       ps->chunk_blocks <= 0 && zbytes <= ((size_t)2 << 30)) {
-    HIPCHK(ps->Z.ensure(zbytes));
+    // (generic N > 256 path: Z holds all K rows — the row FFT makes the channelised
+    // product from them — and the synthesis starts at row `off`)
+    const int64_t z0 = pa->fused ? off : 0;
+    const int64_t zr = K - z0;
+    HIPCHK(ps->Z.ensure((size_t)pa->n_pol * zr * pa->N * sizeof(float2)));
     float2* Z = ps->Z.as<float2>();
-    pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, off);
+    pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zr * pa->N, z0);
     if (st != PFB_OK) return st;
-    return synthesis_blocks(ps, Z, zrows * pa->N, 0, B, (float2*)out, out_ps, olen, s);
+    return synthesis_blocks(ps, Z + (off - z0) * pa->N, zr * pa->N, 0, B, (float2*)out, out_ps,
+                            olen, s);
   }
 
   if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));

@@ -33,6 +33,10 @@ struct AnalysisArgs {
   float2* z;
   int64_t z_pol_stride;
   int64_t z_row0;
+  // generic path (N > 256) with z: the FIR writes only the Z rows (all K of them,
+  // z_row0 = 0) and the row FFT makes the channelised rows from them through this
+  // index reversal (padded variant; null for Bunton) — see fir_window_kernel
+  const int* zrev;
 };
 // analysis kernels that can also emit the synthesis stage-1 rows (see AnalysisArgs::z)
 bool analysis_can_emit_z(const AnalysisArgs& a);
