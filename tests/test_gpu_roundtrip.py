@@ -194,3 +194,47 @@ def test_c2_full_size_linearity(c2):
     lhs = y.cpu().numpy()
     rhs = (a * y1 + b * y2).cpu().numpy()
     assert_pfb_close(lhs, rhs, tol=2e-6, what="linearity")
+
+
+# ------------------------------------------------------------------ BASELINE C3 size
+def test_c3_full_size_impulse_and_linearity(gpu):
+    """BASELINE configs[2] (SKA-Mid padded, 4096 ch, 8/7, 100 353 two-stage taps,
+    2^26 samples, Nf 512, Ov 128) at full size, through the fused generic round trip:
+    size-independent properties instead of the float64 oracle (too slow at 2^26 x 4096):
+    * an impulse comes back as an impulse (TestImpulse.m:46-73: <= -60 dB outside +-1
+      sample), at the padded bank's delay;
+    * the channelised product equals the separate analysis call bit for bit;
+    * linearity of the whole round trip."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
+    assert len(taps) == 100353
+    n = 1 << 26
+    ana = pfb.AnalysisPlan(taps, 4096, "8/7", "polyphase_analysis_padded", 1, 0)
+    win = pfb.PFBWindow().lookup["tukey"](512, 128)
+    syn = pfb.SynthesisPlan(4096, "8/7", 512, 128, True, 1, True, taps, win, None, 1, 0)
+    x = torch.zeros((1, n), dtype=torch.complex64, device=gpu)
+    off = 40_000_000
+    x[0, off] = 1.0
+    chan, y = pfb.roundtrip(ana, syn, x)
+    assert torch.equal(chan, ana.execute(x)), "channelised product differs"
+    yy = y[0].abs().cpu().numpy()
+    pk = int(np.argmax(yy))
+    amp = 20 * np.log10(yy / yy.max() + 1e-30)
+    mask = np.ones(len(yy), bool)
+    mask[max(pk - 1, 0):pk + 2] = False
+    assert amp[mask].max() <= -60.0, amp[mask].max()
+    # delay: the synthesis drops the output overlap Ov de/nu N = 458 752 samples and the
+    # padded bank's -sds row shift centres its (L_h - 1)/2 group delay, so the impulse
+    # comes back within a filter length of off - 458 752
+    assert abs((off - pk) - 458752) <= len(taps), (off, pk, off - pk)
+    # linearity on noise (same plan, different input)
+    g = torch.Generator(device=gpu).manual_seed(3)
+    x1 = torch.complex(torch.randn((1, n), device=gpu, generator=g),
+                       torch.randn((1, n), device=gpu, generator=g)).to(torch.complex64)
+    _, y1 = pfb.roundtrip(ana, syn, x1)
+    y1 = y1.clone()
+    _, y2 = pfb.roundtrip(ana, syn, (x1 * 0.5 + x * 3.0).to(torch.complex64))
+    lhs = y2.cpu().numpy()
+    rhs = (0.5 * y1 + 3.0 * y).cpu().numpy()
+    assert_pfb_close(lhs, rhs, tol=2e-6, what="C3 linearity")
