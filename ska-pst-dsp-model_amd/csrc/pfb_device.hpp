@@ -257,6 +257,28 @@ __device__ __forceinline__ float2 table_tw(const float2* __restrict__ tw, int m)
   return w;
 }
 
+// Twiddles w[r] = e^{DIR 2 pi i r m / N}, r = 1 .. R-1, from log2(R) table reads
+// (r a power of two) and at most 3 complex products for the others (r = highest power of
+// two below r, times the remainder): the reads issue back to back instead of R - 1
+// dependent LDS round trips, at <= 3 roundings of error per twiddle.
+__host__ __device__ constexpr int high_bit(int r) {
+  int h = 1;
+  while (2 * h <= r) h *= 2;
+  return h;
+}
+template <int R, int DIR>
+__device__ __forceinline__ void twiddle_powers(const float2* __restrict__ tw, int m, float2 (&w)[R]) {
+  static_for<1, R>([&](auto rv) {
+    constexpr int r = decltype(rv)::value;
+    if constexpr (high_bit(r) == r) w[r] = table_tw<DIR>(tw, r * m);
+  });
+  static_for<1, R>([&](auto rv) {
+    constexpr int r = decltype(rv)::value;
+    constexpr int h = high_bit(r);
+    if constexpr (h != r) w[r] = cmul(w[h], w[r - h]);
+  });
+}
+
 // One Stockham autosort pass of radix R over `rows` transforms of length N held by
 // the workgroup.  NS = product of the radices already applied.  Loads through `in`,
 // stores through `out`.  All NT threads participate; the pass contains one barrier

@@ -216,7 +216,9 @@ __device__ __forceinline__ void fused_select_pass(const LdsPairs& rowsF, const L
     const int b = tid + p * NTH;
     if (TOT % NTH == 0 || b < TOT) {
       const int q = b % PAIRS, j = b / PAIRS;
-      static_for<1, RL>([&](auto r) { v[p][r] = cmul(v[p][r], table_tw<-1>(twF, r * j)); });
+      float2 w[RL];
+      twiddle_powers<RL, -1>(twF, j, w);
+      static_for<1, RL>([&](auto r) { v[p][r] = cmul(v[p][r], w[r]); });
       sdft<RL, -1>(v[p]);
       cpx2 u[RW1];
       static_for<0, RW1>([&](auto rr) {
