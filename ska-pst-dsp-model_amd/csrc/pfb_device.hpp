@@ -305,10 +305,10 @@ __device__ __forceinline__ void stockham_pass(const In& in, const Out& out,
       const int row = b / NB, j = b - (b / NB) * NB;
       const int k = j % NS;
       if constexpr (NS > 1) {
-        static_for<1, R>([&](auto r) {
-          // e^{DIR 2 pi i r k / (NS R)} = table[(r k N / (NS R))]
-          v[p][r] = cmul(v[p][r], table_tw<DIR>(tw, r * k * (N / (NS * R))));
-        });
+        // e^{DIR 2 pi i r k / (NS R)} = table[(r k N / (NS R))]
+        float2 w[R];
+        twiddle_powers<R, DIR>(tw, k * (N / (NS * R)), w);
+        static_for<1, R>([&](auto r) { v[p][r] = cmul(v[p][r], w[r]); });
       }
       sdft<R, DIR>(v[p]);
       const int idxD = (j / NS) * NS * R + k;
