@@ -434,12 +434,22 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
   hipStream_t s = (hipStream_t)stream;
   const int64_t total = p->buffered + n_in;
   const hipMemcpyKind kin = mem == PFB_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
-  // input = cat(3, input_buffer, input)   (FilterBank.m:85-88)
-  HIPCHK(p->work.ensure((size_t)p->n_pol * std::max<int64_t>(total, 1) * sizeof(float2)));
-  float2* w = p->work.as<float2>();
-  HIPCHK(copy_pols(w, total, p->carry.as<float2>(), p->buffered, p->buffered, p->n_pol,
-                   hipMemcpyDeviceToDevice, s));
-  HIPCHK(copy_pols(w + p->buffered, total, (const float2*)in, in_ps, n_in, p->n_pol, kin, s));
+  // input = cat(3, input_buffer, input)   (FilterBank.m:85-88); with nothing buffered and
+  // the input already on the device the kernels read it in place (no copy)
+  const float2* w;
+  int64_t wps;
+  if (p->buffered == 0 && mem == PFB_MEM_DEVICE) {
+    w = (const float2*)in;
+    wps = in_ps;
+  } else {
+    HIPCHK(p->work.ensure((size_t)p->n_pol * std::max<int64_t>(total, 1) * sizeof(float2)));
+    float2* wk = p->work.as<float2>();
+    HIPCHK(copy_pols(wk, total, p->carry.as<float2>(), p->buffered, p->buffered, p->n_pol,
+                     hipMemcpyDeviceToDevice, s));
+    HIPCHK(copy_pols(wk + p->buffered, total, (const float2*)in, in_ps, n_in, p->n_pol, kin, s));
+    w = wk;
+    wps = total;
+  }
   const int64_t K = analysis_K(p, total);
   PadConsume pad_once{&p->lowcbf_pad};
   const int64_t Kt = K - (K % p->nu);  // trim to a multiple of nu (FilterBank.m:93-104)
@@ -447,22 +457,25 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
   if (Kt > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld rows",
                             (long long)cap, (long long)Kt);
   if (Kt > 0) {
+    // rows are independent except for the padded variant's circular shift over all K
+    // rows: the others compute just the Kt kept rows, straight into the caller's buffer
+    const int64_t Krun = p->variant == pfb::kPadded ? K : Kt;
     float2* dst;
     int64_t dps;
     if (mem == PFB_MEM_HOST) {
-      HIPCHK(p->stage_out.ensure((size_t)p->n_pol * K * p->C * sizeof(float2)));
+      HIPCHK(p->stage_out.ensure((size_t)p->n_pol * Krun * p->C * sizeof(float2)));
       dst = p->stage_out.as<float2>();
-      dps = K * p->C;
+      dps = Krun * p->C;
     } else {
       dst = (float2*)out;
       dps = out_ps;
-      if (Kt != K) {  // kernels write K rows; stage when the caller sized for Kt only
-        HIPCHK(p->stage_out.ensure((size_t)p->n_pol * K * p->C * sizeof(float2)));
+      if (Krun != Kt) {  // padded: K rows computed; stage when the caller sized for Kt only
+        HIPCHK(p->stage_out.ensure((size_t)p->n_pol * Krun * p->C * sizeof(float2)));
         dst = p->stage_out.as<float2>();
-        dps = K * p->C;
+        dps = Krun * p->C;
       }
     }
-    pfb_status st = analysis_run(p, w, total, total, dst, dps, 0, K, K, s);
+    pfb_status st = analysis_run(p, w, wps, total, dst, dps, 0, Krun, K, s);
     if (st != PFB_OK) return st;
     if (dst != (float2*)out) {
       const hipMemcpyKind ko = mem == PFB_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
@@ -475,7 +488,7 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
   if (nb > 0) {
     HIPCHK(p->carry.ensure((size_t)p->n_pol * nb * sizeof(float2)));
     // carry may alias nothing in `work` (separate buffer); copy per pol
-    HIPCHK(copy_pols(p->carry.as<float2>(), nb, w + input_idat, total, nb, p->n_pol,
+    HIPCHK(copy_pols(p->carry.as<float2>(), nb, w + input_idat, wps, nb, p->n_pol,
                      hipMemcpyDeviceToDevice, s));
   }
   p->buffered = std::max<int64_t>(nb, 0);
