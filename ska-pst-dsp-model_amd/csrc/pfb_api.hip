@@ -885,12 +885,22 @@ pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* p, const pfb_cf32*
   const int N = p->N;
   const int64_t total = p->buffered + n_in;
   const hipMemcpyKind kin = mem == PFB_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
-  HIPCHK(p->work.ensure((size_t)p->n_pol * std::max<int64_t>(total, 1) * N * sizeof(float2)));
-  float2* w = p->work.as<float2>();
-  HIPCHK(copy_pols(w, total * N, p->carry.as<float2>(), p->buffered * N, p->buffered * N, p->n_pol,
-                   hipMemcpyDeviceToDevice, s));
-  HIPCHK(copy_pols(w + p->buffered * N, total * N, (const float2*)in, in_ps, n_in * N, p->n_pol, kin,
-                   s));
+  // input = cat(3, input_buffer, input); read in place when nothing is buffered
+  const float2* w;
+  int64_t wps;
+  if (p->buffered == 0 && mem == PFB_MEM_DEVICE) {
+    w = (const float2*)in;
+    wps = in_ps;
+  } else {
+    HIPCHK(p->work.ensure((size_t)p->n_pol * std::max<int64_t>(total, 1) * N * sizeof(float2)));
+    float2* wk = p->work.as<float2>();
+    HIPCHK(copy_pols(wk, total * N, p->carry.as<float2>(), p->buffered * N, p->buffered * N, p->n_pol,
+                     hipMemcpyDeviceToDevice, s));
+    HIPCHK(copy_pols(wk + p->buffered * N, total * N, (const float2*)in, in_ps, n_in * N, p->n_pol,
+                     kin, s));
+    w = wk;
+    wps = total * N;
+  }
   // output length and carry-over rounded up to a multiple of nu (InverseFilterBank.m:104-135)
   const int64_t B = synth_blocks(p, total);
   const int64_t full = B * p->Lkeep;
@@ -911,18 +921,18 @@ pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* p, const pfb_cf32*
   if (olen > 0) {
     if (mem == PFB_MEM_HOST) {
       HIPCHK(p->stage_out.ensure((size_t)p->n_pol * olen * sizeof(float2)));
-      pfb_status st = synthesis_run(p, w, total * N, total, p->stage_out.as<float2>(), olen, olen, s);
+      pfb_status st = synthesis_run(p, w, wps, total, p->stage_out.as<float2>(), olen, olen, s);
       if (st != PFB_OK) return st;
       HIPCHK(copy_pols((float2*)out, out_ps, p->stage_out.as<float2>(), olen, olen, p->n_pol,
                        hipMemcpyDeviceToHost, s));
     } else {
-      pfb_status st = synthesis_run(p, w, total * N, total, (float2*)out, out_ps, olen, s);
+      pfb_status st = synthesis_run(p, w, wps, total, (float2*)out, out_ps, olen, s);
       if (st != PFB_OK) return st;
     }
   }
   if (buffered > 0) {
     HIPCHK(p->carry.ensure((size_t)p->n_pol * buffered * N * sizeof(float2)));
-    HIPCHK(copy_pols(p->carry.as<float2>(), buffered * N, w + input_idat * N, total * N, buffered * N,
+    HIPCHK(copy_pols(p->carry.as<float2>(), buffered * N, w + input_idat * N, wps, buffered * N,
                      p->n_pol, hipMemcpyDeviceToDevice, s));
   }
   p->buffered = std::max<int64_t>(buffered, 0);
