@@ -318,6 +318,8 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
                 d->os_de);
   if (!d->taps || d->n_taps <= 0) return fail(PFB_ERR_INVALID_ARG, "no filter taps");
   if (d->n_pol <= 0) return fail(PFB_ERR_INVALID_ARG, "n_pol must be positive");
+  if (d->n_pol > 65535)  // polarisations map to grid.y of every launch
+    return fail(PFB_ERR_INVALID_ARG, "n_pol = %d exceeds 65535 series per plan", d->n_pol);
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(PFB_ERR_NO_DEVICE, "no HIP device available");
@@ -642,6 +644,8 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
             Ov = d->input_overlap;
   if (N <= 0 || nu <= 0 || de <= 0 || Nf <= 0 || Ov < 0 || d->n_pol <= 0)
     return fail(PFB_ERR_INVALID_ARG, "invalid synthesis parameters");
+  if (d->n_pol > 65535)  // polarisations map to grid.y of every launch
+    return fail(PFB_ERR_INVALID_ARG, "n_pol = %d exceeds 65535 series per plan", d->n_pol);
   if (((int64_t)Nf * de) % nu != 0)
     return fail(PFB_ERR_INVALID_ARG, "input_fft_length*de/nu = %d*%d/%d is not integral", Nf, de, nu);
   if (((int64_t)Ov * de * N) % nu != 0)
