@@ -351,3 +351,26 @@ def test_purity_impulse_and_tone_through_dada_pipeline(gpu, tmp_path):
     span = (len(y2) // 16384) * 16384
     score = verify.tone_purity(y2[:span])
     assert score["max_spurious"] <= -60.0, score
+
+
+def test_purity_sweep_ska_mid(gpu):
+    """A reduced BASELINE configs[4] sweep (SKA-Mid padded, 4096 ch, 100 353 taps, 3
+    blocks = 5 505 024 samples per vector) through verify.purity_sweep: impulses meet
+    TestImpulse.m's -60 dB outside +-1 sample, the first grid tone (an integral number
+    of periods) TestPureTone.m's -60 dB, the 32-tone comb TestFrequencyComb.m, and the
+    round trip keeps the power of every vector."""
+    from ska_pst_dsp_model_amd import verify
+    recs = verify.purity_sweep(npoints=2, batch=6)
+    kinds = [r["kind"] for r in recs]
+    assert kinds.count("impulse") == 2 and kinds.count("tone") == 2
+    for r in recs:
+        if r["kind"] == "impulse":
+            assert r["max_outside_pm1_dB"] <= -60.0, r
+            assert abs(r["peak_index"] - r["expected_index"]) < 100353, r
+        elif r["kind"] == "comb":
+            assert r["comb_test"] == 0, r
+        elif r["kind"] in ("square_wave",):
+            assert 0.9 < r["power_ratio"] < 1.1, r
+    tone0 = [r for r in recs if r["kind"] == "tone"][0]
+    assert tone0["param"] == 3 and tone0["max_spurious"] <= -60.0, tone0
+    assert 0.95 < tone0["power_ratio"] < 1.05, tone0
