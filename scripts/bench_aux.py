@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--skip-mid", action="store_true")
     ap.add_argument("--only-mid", action="store_true")
+    ap.add_argument("--cpu", action="store_true",
+                    help="also time the NumPy oracle (1 core) on bounded samples of each config")
     args = ap.parse_args()
     import torch
     import ska_pst_dsp_model_amd as pfb
@@ -57,6 +59,8 @@ def main():
         return torch.complex(torch.randn(shape, device=dev, generator=g),
                              torch.randn(shape, device=dev, generator=g)).to(torch.complex64)
 
+    if args.cpu:
+        cpu_baselines(pfb)
     if args.only_mid:
         return mid(torch, pfb, noise, dev)
     # ---- C2' (4/3) round trip
@@ -119,6 +123,46 @@ def main():
         del x, x2, raw8, raw32, y, rows, chan, out
         torch.cuda.empty_cache()
         mid(torch, pfb, noise, dev)
+
+
+def cpu_baselines(pfb):
+    """The reference's CPU path stand-in (the NumPy oracle, complex64 where Matlab uses
+    single, numpy.fft single-threaded) on bounded samples of the other configurations."""
+    import time
+    from oracle import pfb_oracle as orc
+    rng = np.random.default_rng(0)
+
+    def noise(n, n_pol=1):
+        return ((rng.standard_normal((n_pol, 1, n)) + 1j * rng.standard_normal((n_pol, 1, n))) /
+                np.sqrt(2)).astype(np.complex64)
+
+    def timed(fn, samples, what, sample):
+        t0 = time.perf_counter()
+        fn()
+        el = time.perf_counter() - t0
+        print(json.dumps({"cpu": what, "msamples_per_s": round(samples / el / 1e6, 3),
+                          "cores": 1, "kind": "port", "sample": sample,
+                          "seconds": round(el, 2)}), flush=True)
+
+    taps43 = pfb.design_PFB_FIR_filter(256, "4/3", 12)
+    x = noise(1 << 20)
+    win = orc.pfb_window("tukey", 256, 48)
+    dr = {"apply_deripple": 1, "filter_coeff": taps43}
+    timed(lambda: orc.polyphase_synthesis(
+        orc.polyphase_analysis(x, taps43, 256, "4/3", dtype=np.complex64), 1, 256, "4/3", dr, 1,
+        48, win, dtype=np.complex64), 1 << 20, "C2' round trip", "2^20 samples")
+    pst = pfb.read_fir_filter_coeff(os.path.join(pfb.config.config_dir, "PST_filtertaps.txt"))
+    x2 = noise(1 << 18, 2)
+    timed(lambda: orc.polyphase_analysis_lowcbf(x2, pst, do_padding=False), 2 << 18,
+          "LowCBF PST filterbank", "2 pol x 2^18 samples")
+    tm = pfb.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
+    x3 = noise(1 << 22)
+    winm = orc.pfb_window("tukey", 512, 128)
+    drm = {"apply_deripple": 1, "filter_coeff": tm}
+    timed(lambda: orc.polyphase_synthesis(
+        orc.polyphase_analysis_padded(x3, tm, 4096, "8/7", dtype=np.complex64), 1, 512, "8/7",
+        drm, 1, 128, winm, dtype=np.complex64), 1 << 22, "C3 SKA-Mid round trip",
+        "2^22 samples (2 synthesis blocks)")
 
 
 def mid(torch, pfb, noise, dev, reps=3):
