@@ -250,6 +250,10 @@ pfb_status pfb_device_free(void* ptr);
 pfb_status pfb_memcpy_h2d(void* dst, const void* src, int64_t bytes, void* stream);
 pfb_status pfb_memcpy_d2h(void* dst, const void* src, int64_t bytes, void* stream);
 pfb_status pfb_stream_synchronize(void* stream);
+/* Bandwidth probe (no reference counterpart; SURVEY §8(d) asks for the achievable
+ * copy rate beside the HBM spec): device-to-device float4 copy kernel.  16-B aligned
+ * pointers, n_bytes a multiple of 64.  Asynchronous on `stream`. */
+pfb_status pfb_device_copy(void* dst, const void* src, int64_t n_bytes, void* stream);
 
 /* Kernel timing: average duration (ms) of the named kernel class over the launches
  * recorded since the last reset, measured with HIP events on the plan's stream.

@@ -14,7 +14,7 @@ import sys
 
 
 def short(name):
-    for k in ("analysis_fused", "analysis_stream", "row_fft", "synth_block", "fir_generic"):
+    for k in ("analysis_fused", "analysis_stream", "row_fft", "synth_block", "fir_generic", "fir_window"):
         if k in name:
             return name.split("(")[0].replace("void pfb::", "")
     return None

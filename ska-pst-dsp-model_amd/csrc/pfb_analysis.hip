@@ -326,15 +326,25 @@ __global__ __launch_bounds__(NT) void fir_generic_kernel(AnalysisArgs a) {
 // arm n in registers and loads only the DE new ones per row (instead of P): the L2 read
 // traffic of the FIR drops by P / DE (3.6x on C3).  The circular-shift position of arm
 // n depends only on k mod NU (= s), so each thread writes one fixed column.
-template <int PW, int DE, int VARIANT>
-__global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int ranges) {
+template <int PW, int DE, int VARIANT, int U = 1>
+__global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int ranges, int slice_map) {
   const int N = a.N, M = a.M, NU = a.nu;
   const int chunks = N / NT;
   int bid = blockIdx.x;
-  const int chunk = bid % chunks;
+  const int d = bid % chunks;
   bid /= chunks;
   const int s = bid % NU;
   const int rg = bid / NU;
+  // Residue s reads input columns (s M + n) mod N (Bunton) / (s M - 1 - n) mod N (padded)
+  // of every N-sample row: with M a multiple of NT, the NU residues of one column slice d
+  // are NU different thread chunks.  The fast block index is the slice d, so all blocks
+  // reading slice d share blockIdx mod 8, i.e. one XCD and its L2 (chunk-major order
+  // spreads each slice over 4 XCDs: 4.7x the input read from HBM on C3).
+  int chunk = d;
+  if (slice_map) {
+    const int sh = (int)(((int64_t)s * M % N) / NT);
+    chunk = VARIANT == kBunton ? (d - sh + chunks) % chunks : ((sh - 1 - d) % chunks + chunks) % chunks;
+  }
   const int pol = blockIdx.y;
   const int n = chunk * NT + threadIdx.x;
   // rows of residue s in [row0, K): k = s + NU j, j in [jlo, jhi)
@@ -362,9 +372,6 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
   auto gidx = [&](int64_t k, int p) -> int64_t {
     return VARIANT == kBunton ? k * M + (int64_t)p * N + n : k * M - 1 - (int64_t)p * N - n;
   };
-  v2f w[PW];
-#pragma unroll
-  for (int p = 0; p < PW; ++p) w[p] = ld(gidx(kfirst, p));
   int pos;
   if constexpr (VARIANT == kBunton) {
     pos = (int)((n + ((int64_t)s * M) % N) % N);
@@ -380,6 +387,67 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
   float2* zc = a.z ? a.z + pol * a.z_pol_stride + (VARIANT == kBunton ? pos : (N - pos) % N)
                    : nullptr;
   const float zscale = (float)N * (float)N;
+  auto emit = [&](int64_t k, v2f acc) {
+    if (!zc) sc[(k - a.row0) * N] = make_float2(acc.x, acc.y);
+    if (zc) {
+      int64_t t = k;
+      if constexpr (VARIANT != kBunton) {
+        t = k - a.sds;
+        while (t < 0) t += a.K_total;
+      }
+      if (t >= a.z_row0) zc[(t - a.z_row0) * N] = make_float2(zscale * acc.x, zscale * acc.y);
+    }
+  };
+  if constexpr (U > 1) {
+    // U rows per iteration, their U DE new samples loaded together one iteration ahead:
+    // a thread waits once per U rows and moves PW + (U-1) DE window registers per U rows
+    // instead of PW + DE per row (C3, measured: U = 1 517 us, 2 487 us, 3 540 us — three
+    // waves per SIMD at U = 2 and 3 instead of four; a move-free ring window with one or
+    // two rows of loads ahead, 491 / 510 us, was no better).  Extended window X[i] = the sample of arm q(i) of row
+    // k + (U-1) NU, q = i (padded) / PW-1-i (Bunton); arm p of row k + u NU is
+    // X[(U-1-u) DE + q(p)], and the next iteration's window is X shifted by U DE.
+    constexpr int XS = PW + (U - 1) * DE;
+    v2f X[XS];
+#pragma unroll
+    for (int i = 0; i < XS; ++i) {
+      const int u = i >= (U - 1) * DE ? 0 : U - 1 - i / DE;
+      const int q = i - (U - 1 - u) * DE;
+      X[i] = ld(gidx(kfirst + (int64_t)u * NU, VARIANT == kBunton ? PW - 1 - q : q));
+    }
+#pragma unroll 1
+    for (int64_t j = j0; j < j1; j += U) {
+      const int64_t k = s + (int64_t)NU * j;
+      v2f L[U * DE];
+#pragma unroll
+      for (int i = 0; i < U * DE; ++i) {
+        const int u = 2 * U - 1 - i / DE, q = i % DE;
+        L[i] = ld(gidx(k + (int64_t)u * NU, VARIANT == kBunton ? PW - 1 - q : q));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        // same arm order and pairing as the U = 1 loop (bit-identical sums)
+        v2f acc0{0.f, 0.f}, acc1{0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < PW; p += 2) {
+          const int i0 = (U - 1 - u) * DE + (VARIANT == kBunton ? PW - 1 - p : p);
+          acc0 = __builtin_elementwise_fma(v2f{f[p], f[p]}, X[i0], acc0);
+          if (p + 1 < PW) {
+            const int i1 = (U - 1 - u) * DE + (VARIANT == kBunton ? PW - 2 - p : p + 1);
+            acc1 = __builtin_elementwise_fma(v2f{f[p + 1], f[p + 1]}, X[i1], acc1);
+          }
+        }
+        if (j + u < j1) emit(k + (int64_t)u * NU, acc0 + acc1);
+      }
+#pragma unroll
+      for (int i = XS - 1; i >= U * DE; --i) X[i] = X[i - U * DE];
+#pragma unroll
+      for (int i = 0; i < U * DE; ++i) X[i] = L[i];
+    }
+    return;
+  }
+  v2f w[PW];
+#pragma unroll
+  for (int p = 0; p < PW; ++p) w[p] = ld(gidx(kfirst, p));
 #pragma unroll 1
   for (int64_t j = j0; j < j1; ++j) {
     const int64_t k = s + (int64_t)NU * j;
@@ -394,16 +462,7 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
       acc0 = __builtin_elementwise_fma(v2f{f[p], f[p]}, w[p], acc0);
       if (p + 1 < PW) acc1 = __builtin_elementwise_fma(v2f{f[p + 1], f[p + 1]}, w[p + 1], acc1);
     }
-    const v2f acc = acc0 + acc1;
-    if (!zc) sc[(k - a.row0) * N] = make_float2(acc.x, acc.y);
-    if (zc) {
-      int64_t t = k;
-      if constexpr (VARIANT != kBunton) {
-        t = k - a.sds;
-        while (t < 0) t += a.K_total;
-      }
-      if (t >= a.z_row0) zc[(t - a.z_row0) * N] = make_float2(zscale * acc.x, zscale * acc.y);
-    }
+    emit(k, acc0 + acc1);
     if constexpr (VARIANT == kBunton) {
 #pragma unroll
       for (int p = 0; p < PW - DE; ++p) w[p] = w[p + DE];
@@ -422,12 +481,29 @@ template <int PW, int DE>
 static hipError_t launch_fir_window_t(const AnalysisArgs& a, hipStream_t s) {
   const int chunks = a.N / NT;
   const int base = chunks * a.nu * a.n_pol;
-  const int ranges = std::max(1, (4 * 1024 + base - 1) / base);
+  static const int target = [] {
+    const char* v = std::getenv("PFB_FIR_BLOCKS");
+    return v ? std::max(1, std::atoi(v)) : 4 * 1024;
+  }();
+  static const int rows = [] {
+    const char* v = std::getenv("PFB_FIR_ROWS");
+    return v ? std::atoi(v) : 2;
+  }();
+  static const bool no_map = std::getenv("PFB_FIR_NO_SLICE_MAP") != nullptr;
+  const int slice_map = !no_map && a.M % NT == 0;
+  const int ranges = std::max(1, (target + base - 1) / base);
   dim3 grid((unsigned)(chunks * a.nu * ranges), (unsigned)a.n_pol);
-  if (a.variant == kBunton)
-    hipLaunchKernelGGL((fir_window_kernel<PW, DE, kBunton>), grid, dim3(NT), 0, s, a, ranges);
-  else
-    hipLaunchKernelGGL((fir_window_kernel<PW, DE, kPadded>), grid, dim3(NT), 0, s, a, ranges);
+  auto go = [&](auto u) {
+    // (wide DE: the U DE loads in flight would not fit the register budget)
+    constexpr int U = DE * decltype(u)::value <= 21 ? decltype(u)::value : 1;
+    if (a.variant == kBunton)
+      hipLaunchKernelGGL((fir_window_kernel<PW, DE, kBunton, U>), grid, dim3(NT), 0, s, a, ranges, slice_map);
+    else
+      hipLaunchKernelGGL((fir_window_kernel<PW, DE, kPadded, U>), grid, dim3(NT), 0, s, a, ranges, slice_map);
+  };
+  if (rows == 1) go(std::integral_constant<int, 1>{});
+  else if (rows == 2) go(std::integral_constant<int, 2>{});
+  else go(std::integral_constant<int, 3>{});
   return hipGetLastError();
 }
 

@@ -114,6 +114,7 @@ SYMBOLS = [
     ("pfb_memcpy_h2d", c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     ("pfb_memcpy_d2h", c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     ("pfb_stream_synchronize", c_int32, [c_void_p]),
+    ("pfb_device_copy", c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     ("pfb_profile_enable", c_int32, [c_int32]),
     ("pfb_profile_read", c_int32, [c_int32, POINTER(c_double), POINTER(c_int64),
                                    POINTER(c_double)]),

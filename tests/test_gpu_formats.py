@@ -125,6 +125,22 @@ def test_gather_rejects_out_of_row(gpu):
                                n_sel=8, shift=1, split=4)
 
 
+def test_device_copy_probe(gpu):
+    """bench.py's bandwidth probe copies exactly (ragged tail of a block) and rejects
+    misaligned sizes."""
+    import torch
+    from ska_pst_dsp_model_amd import _lib
+    lib = _lib.load()
+    n = 4 * 1024 * 5 + 16 * 7                      # floats: 5 blocks + a partial one
+    src = torch.arange(n, dtype=torch.float32, device=gpu)
+    dst = torch.zeros(n + 16, dtype=torch.float32, device=gpu)
+    s = torch.cuda.current_stream(gpu).cuda_stream
+    assert lib.pfb_device_copy(dst.data_ptr(), src.data_ptr(), n * 4, s) == 0
+    torch.cuda.synchronize(gpu)
+    assert torch.equal(dst[:n], src) and not dst[n:].any()
+    assert lib.pfb_device_copy(dst.data_ptr(), src.data_ptr(), 40, s) != 0
+
+
 # ----------------------------------------------------------------------------- quantisation
 def test_quantize_round_half_away(gpu):
     import torch
