@@ -189,6 +189,18 @@ __device__ __forceinline__ void load_t4(v4f (&t4)[(PAIRS * NBL + NTH - 1) / NTH]
   });
 }
 
+// the same from the workgroup's LDS copy of its TG columns of the table ([j'][pair q])
+template <int NBL, int RW1, int PAIRS, int NTH>
+__device__ __forceinline__ void load_t4_lds(v4f (&t4)[(PAIRS * NBL + NTH - 1) / NTH][RW1],
+                                            const v4f* t4l, int tid) {
+  constexpr int TOT = PAIRS * NBL;
+  static_for<0, (TOT + NTH - 1) / NTH>([&](auto p) {
+    const int b = min(tid + p * NTH, TOT - 1);
+    const int q = b % PAIRS, j = b / PAIRS;
+    static_for<0, RW1>([&](auto rr) { t4[p][rr] = t4l[(j + NBL * rr) * PAIRS + q]; });
+  });
+}
+
 // Last Nf-point pass (forward, radix RL, NS = NBL) + kept-bin selection + gain x
 // twiddle + first W-point pass (inverse, radix RW1, NS = 1), LDS rowsF -> LDS rowsW
 // (in place; one barrier between the loads and the stores).
@@ -237,7 +249,11 @@ __device__ __forceinline__ void fused_select_pass(const LdsPairs& rowsF, const L
 // first-pass register r of a thread holds row j + r NF/R1 — so the next block's
 // registers 0 .. R1-DK-1 are this block's registers DK .. R1-1: they move in registers
 // and only DK of the R1 rows are read from HBM (the 2 Ov overlap re-read disappears).
-template <int NF, int W, int PAIRS, bool SPANS, bool PERSIST, int DK = 0, bool P16 = false>
+// T4L: the workgroup's TG columns of the gain x twiddle table are copied to LDS once
+// and read from there every block (SKA-Mid: the 14.7 MB table was re-read from L2/MALL
+// for each of a workgroup's blocks; only where the copy keeps 4 workgroups per CU).
+template <int NF, int W, int PAIRS, bool SPANS, bool PERSIST, int DK = 0, bool P16 = false,
+          bool T4L = false>
 __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void synth_block_kernel(SynthBlockArgs a) {
   using SS = SynthPairShape<NF, W, PAIRS>;
   using SP = SynthPlan<NF, W>;
@@ -273,6 +289,13 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
   const uint32_t zbytes = (a.timing_mask & 1) ? 0u : (uint32_t)((NF - 1) * N + TG) * 8u;
   const uint32_t twbytes = (a.timing_mask & 4) ? 0u : (uint32_t)((W - 1) * N + TG) * 8u;
   const __amdgpu_buffer_rsrc_t tw4r = make_rsrc(a.tw4 + t0, twbytes);
+  v4f* t4l = reinterpret_cast<v4f*>(reinterpret_cast<char*>(smem) + SS::lds_bytes);
+  if constexpr (T4L) {
+    for (int i = tid; i < W * PAIRS; i += NTP) {
+      const int jr = i / PAIRS, q = i % PAIRS;
+      t4l[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(tw4r, (jr * N + 2 * q) * 8, 0, 0));
+    }
+  }
   const LdsPairs rowsF{reinterpret_cast<v4f*>(smem), SS::RSF};
   const LdsPairs rowsW{reinterpret_cast<v4f*>(smem), SS::RSW};
   float2* opol = a.out + pol * a.out_pol_stride;
@@ -307,7 +330,8 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
       // the gain x twiddle loads go out BEFORE the next block's prefetch: vmcnt retires
       // in order, so waiting for them must not mean waiting for the HBM prefetch too
       v4f t4[PT][RW1];
-      load_t4<NBL, RW1, PAIRS, NTP>(t4, tw4r, N, tid);
+      if constexpr (T4L) load_t4_lds<NBL, RW1, PAIRS, NTP>(t4, t4l, tid);
+      else load_t4<NBL, RW1, PAIRS, NTP>(t4, tw4r, N, tid);
       after_first();
       __syncthreads();
       if constexpr (!std::is_same_v<typename SP::Mid, Radices<>>) {
@@ -368,13 +392,21 @@ static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
     constexpr bool FU = SynthPlan<NF, W>::fused;
     const bool reuse = DK > 0 && a.keep == DK * NB1 && !a.no_reuse;
     const bool p16 = (a.out_limit % 2 == 0) && (a.Lkeep % 2 == 0);
-    auto kern = reuse ? (p16 ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true>
+    // table copy in LDS where it still leaves 4 two-wave workgroups per CU (the VGPR
+    // limit): SKA-Mid 25.7 + 14 KB; not SKA-Low (38.5 + 28 KB)
+    constexpr size_t t4_bytes = (size_t)W * PAIRS * 16;
+    constexpr bool T4 = SS::lds_bytes + t4_bytes <= (160 * 1024) / 4;
+    static const bool no_t4l = std::getenv("PFB_SYNTH_NO_T4LDS") != nullptr;
+    const bool t4l = T4 && !no_t4l && reuse && p16;
+    const size_t lds = SS::lds_bytes + (t4l ? t4_bytes : 0);
+    auto kern = t4l ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true, T4>
+              : reuse ? (p16 ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true>
                              : synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, false>)
                       : (p16 ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, 0, true>
                              : synth_block_kernel<NF, W, PAIRS, SPANS, FU, 0, false>);
-    hipError_t e = set_lds(kern, SS::lds_bytes);
+    hipError_t e = set_lds(kern, lds);
     if (e != hipSuccess) return e;
-    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / SS::lds_bytes));
+    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / lds));
     // resident-capacity ranges; when that leaves more than 16 blocks per range (many
     // phase groups per block row: SKA-Mid N / TG = 1024 gives one range of 72 blocks),
     // ranges of 6 blocks instead (oversubscribed, evenly split): C3 1.59 -> 1.51 ms.
@@ -386,7 +418,7 @@ static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
     }
     ranges = std::min(ranges, a.n_blocks);
     dim3 grid((unsigned)(groups * ranges), (unsigned)a.n_pol);
-    return launch_kernel(kern, grid, dim3(NTP), SS::lds_bytes, s, a);
+    return launch_kernel(kern, grid, dim3(NTP), lds, s, a);
   }
   auto kern = synth_block_kernel<NF, W, PAIRS, SPANS, false>;
   hipError_t e = set_lds(kern, SS::lds_bytes);
