@@ -178,16 +178,27 @@ pfb_status pfb_synthesis_set_chunk_blocks(pfb_synthesis_plan* plan, int32_t bloc
  * Device memory only.  in: n_pol series of n_dat samples; chan: the full channelised
  * product (n_pol x K x n_chan, written as pfb_analysis_execute writes it); out: the
  * synthesis of chan(:, :, sample_offset:end) as pfb_synthesis_execute computes it.
- * Internally pipelined in chunks of synthesis blocks (pfb_synthesis_set_chunk_blocks,
- * default 64) with the analysis on a second stream; results are bit-identical to the
- * two separate calls.  Ordered after prior work on `stream`; later work on `stream`
- * sees all of it (graph-capturable). */
+ * When the analysis kernel can emit the synthesis stage-1 rows (N = 256 streaming
+ * shapes, the N > 256 register-window FIR) and no chunk size is set, the two run fused:
+ * `chan` is bit-identical to pfb_analysis_execute and `out` agrees with
+ * pfb_synthesis_execute to ~1e-7 (the stage-1 rows are N^2 x the FIR sums, the exact
+ * channel IFFT of the unrounded row).  Otherwise the call is pipelined in chunks of
+ * synthesis blocks (pfb_synthesis_set_chunk_blocks, default 64) with the analysis on a
+ * second stream, and both results are bit-identical to the separate calls.  Ordered
+ * after prior work on `stream`; later work on `stream` sees all of it (graph-capturable). */
 pfb_status pfb_roundtrip_execute(pfb_analysis_plan* analysis, pfb_synthesis_plan* synthesis,
                                  const pfb_cf32* in, int64_t in_pol_stride, int64_t n_dat,
                                  pfb_cf32* chan, int64_t chan_pol_stride, int64_t chan_capacity,
                                  int64_t* n_chan_rows, int64_t sample_offset, pfb_cf32* out,
                                  int64_t out_pol_stride, int64_t out_capacity, int64_t* n_out,
                                  void* stream);
+
+/* Round-trip output length estimate — replaces calc_output_nbins(nbins, channels,
+ * os_factor, filter_taps, input_fft_length, input_overlap) (calc_output_nbins.m:17-27):
+ * Matlab double arithmetic with its floor()s, so a non-integral normalize(os, n) gives the
+ * same fractional result Matlab does.  Host-only arithmetic (no device needed). */
+double pfb_calc_output_nbins(int64_t nbins, int32_t channels, int32_t os_nu, int32_t os_de,
+                             int64_t filter_taps, int32_t input_fft_length, int32_t input_overlap);
 
 /* ---------------------------------------------------------------- data formats */
 /* Sample order of a DADA file's data section. */

@@ -200,7 +200,9 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
   const int64_t row_first = (int64_t)DE * (q_lo + st0 * QS);
   const float2* xpol = a.in + pol * a.in_pol_stride;
   const int64_t avail = a.n_dat - row_first * N;
-  uint32_t nbytes = (uint32_t)min(max(avail, (int64_t)0) * 8, (int64_t)0x7ffffff0);
+  // the launcher sizes the ranges so that a workgroup's rows span <= kRsrcMaxBytes
+  // (launch_stream); the min() only bounds the series tail beyond the range
+  uint32_t nbytes = (uint32_t)min(max(avail, (int64_t)0) * 8, kRsrcMaxBytes);
   if (a.timing_mask & 1) nbytes = 0;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(xpol + row_first * N, nbytes);
   // rows past the last window of the range (the unconditional last prefetch) re-read the
@@ -363,8 +365,9 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
   b0 = max(b0, (int64_t)0);
   const float2* xpol = a.in + pol * a.in_pol_stride;
   const int64_t avail = a.n_dat - b0;
+  // (launch_fir_window_t sizes the ranges so that one range spans <= kRsrcMaxBytes)
   const __amdgpu_buffer_rsrc_t xr =
-      make_rsrc(xpol + b0, (uint32_t)min(max(avail, (int64_t)0) * 8, (int64_t)0x7ffffff0));
+      make_rsrc(xpol + b0, (uint32_t)min(max(avail, (int64_t)0) * 8, kRsrcMaxBytes));
   auto ld = [&](int64_t g) {
     const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (uint32_t)((g - b0) * 8), 0, 0);
     return __builtin_bit_cast(v2f, v);
@@ -491,7 +494,18 @@ static hipError_t launch_fir_window_t(const AnalysisArgs& a, hipStream_t s) {
   }();
   static const bool no_map = std::getenv("PFB_FIR_NO_SLICE_MAP") != nullptr;
   const int slice_map = !no_map && a.M % NT == 0;
-  const int ranges = std::max(1, (target + base - 1) / base);
+  int ranges = std::max(1, (target + base - 1) / base);
+  // one range of residue s reads input samples [k_first M - (PW + 1) N, k_last M + PW N]:
+  // keep that within one buffer descriptor (huge single series: more, shorter ranges)
+  const int64_t rows_s = (a.K - a.row0 + a.nu - 1) / a.nu + 1;
+  const int64_t halo = ((int64_t)PW + 2) * a.N + (int64_t)a.nu * a.M;
+  const int64_t fit = kRsrcMaxBytes / 8 - halo;  // samples of row advance one range may span
+  if (fit <= 0) return hipErrorInvalidValue;
+  const int64_t need = (rows_s * a.nu * a.M + fit - 1) / fit;
+  if (need > ranges) {
+    if (need * chunks * a.nu > INT32_MAX) return hipErrorInvalidValue;
+    ranges = (int)need;
+  }
   dim3 grid((unsigned)(chunks * a.nu * ranges), (unsigned)a.n_pol);
   auto go = [&](auto u) {
     // (wide DE: the U DE loads in flight would not fit the register budget)
@@ -563,7 +577,12 @@ static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
   static const int env_wpc = std::getenv("PFB_ANA_WG_PER_CU") ? std::atoi(std::getenv("PFB_ANA_WG_PER_CU")) : 0;
   if (env_wpc > 0) per_cu = env_wpc;
   const int64_t per_pol = std::max<int64_t>(1, (per_cu * cu_count()) / a.n_pol);
-  const int64_t wgs = std::min<int64_t>(n_steps, per_pol);
+  int64_t wgs = std::min<int64_t>(n_steps, per_pol);
+  // a workgroup's rows (its steps' NEW rows each + the WIN-row window) must fit one
+  // buffer descriptor: huge single series get more, shorter ranges
+  const int64_t fit_steps = (kRsrcMaxBytes / (8 * N) - SH::WIN) / SH::NEW;
+  wgs = std::max(wgs, (n_steps + fit_steps - 1) / fit_steps);
+  if (wgs > INT32_MAX) return hipErrorInvalidValue;
   dim3 grid((unsigned)wgs, (unsigned)a.n_pol);
   return launch_kernel(kern, grid, dim3(NT), SH::lds_bytes, s, a);
 }

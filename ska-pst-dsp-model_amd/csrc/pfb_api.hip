@@ -662,7 +662,13 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
     return fail(PFB_ERR_UNSUPPORTED, "no channel-IFFT kernel for n_chan=%d", N);
   if (!pfb::synth_block_supported(Nf, W))
     return fail(PFB_ERR_UNSUPPORTED, "no synthesis kernel for Nf=%d W=%d", Nf, W);
-  if ((int64_t)W * N >= (1LL << 30)) return fail(PFB_ERR_UNSUPPORTED, "L too large");
+  // the block kernel's buffer descriptors span one block's output (L_keep samples), the
+  // gain x twiddle table (L values) and one block's stage-1 rows (Nf x N): each must fit
+  // one 32-bit descriptor extent (pfb::kRsrcMaxBytes) — rejected here, never clamped
+  if ((int64_t)W * N * 8 > pfb::kRsrcMaxBytes || (int64_t)Nf * N * 8 > pfb::kRsrcMaxBytes)
+    return fail(PFB_ERR_UNSUPPORTED,
+                "output_fft_length %lld or Nf x n_chan %lld exceeds a buffer descriptor "
+                "(%lld bytes)", (long long)W * N, (long long)Nf * N, (long long)pfb::kRsrcMaxBytes);
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(PFB_ERR_NO_DEVICE, "no HIP device available");
@@ -959,8 +965,9 @@ pfb_status pfb_inverse_filterbank_reset(pfb_synthesis_plan* p) {
 // on the caller's stream, so the two kernels share the chip (each alone leaves HBM and
 // VALU partly idle), and the synthesis reads each channelised row shortly after it was
 // written (Infinity-Cache resident).  The full channelised product is still written to
-// `chan`.  Every row and block is computed by the same kernels with the same inputs as
-// pfb_analysis_execute + pfb_synthesis_execute, so the results are bit-identical.
+// `chan`.  On this chunked path every row and block is computed by the same kernels with
+// the same inputs as pfb_analysis_execute + pfb_synthesis_execute, so both results are
+// bit-identical to the separate calls (the fused path below: see its comment).
 pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, const pfb_cf32* in,
                                  int64_t in_ps, int64_t n_dat, pfb_cf32* chan, int64_t chan_ps,
                                  int64_t chan_cap, int64_t* n_chan_rows, int64_t sample_offset,
@@ -995,21 +1002,22 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
   float2* y = (float2*)chan;
   if (B == 0) return analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s);
 
-  // Fused: the analysis kernel also runs the synthesis channel IFFT on every row it
-  // produces (same arithmetic on the same float values, so the output is bit-identical
-  // to the separate calls) and the block kernel reads those rows — the channelised
-  // product is still written in full.  Needs the streaming analysis kernel, no combine
-  // permutation / per-channel gain, and scratch for all K - off rows (bounded at 2 GiB;
-  // an explicit chunk size keeps the chunked pipeline below).
+  // Fused: the analysis kernel also writes the synthesis stage-1 rows (the channel IFFT
+  // of every row it produces, taken as N^2 x its FIR sums before the FFT rather than from
+  // the rounded channelised row — equal in exact arithmetic, so the output agrees with
+  // the separate calls to ~1e-7, not bit for bit) and the block kernel reads them; the
+  // channelised product is still written in full (and IS bit-identical).  Needs an
+  // analysis kernel that can emit the rows, no combine permutation / per-channel gain,
+  // and device memory for the rows (bounded at 16 GiB; an explicit chunk size, or a
+  // larger call, takes the chunked pipeline below).
   static const bool no_fuse = std::getenv("PFB_RT_NO_FUSE") != nullptr;
-  const int64_t zrows = K - off;
-  const size_t zbytes = (size_t)pa->n_pol * zrows * pa->N * sizeof(float2);
+  // (generic N > 256 path: Z holds all K rows — the row FFT makes the channelised product
+  // from them — and the synthesis starts at row `off`; streaming kernel: K - off rows)
+  const int64_t z0 = pa->fused ? off : 0;
+  const int64_t zr = K - z0;
+  const size_t zbytes = (size_t)pa->n_pol * zr * pa->N * sizeof(float2);
   if (!no_fuse && analysis_emits_z(pa) && ps->identity_perm && !ps->has_cgain &&
-      ps->chunk_blocks <= 0 && zbytes <= ((size_t)2 << 30)) {
-    // (generic N > 256 path: Z holds all K rows — the row FFT makes the channelised
-    // product from them — and the synthesis starts at row `off`)
-    const int64_t z0 = pa->fused ? off : 0;
-    const int64_t zr = K - z0;
+      ps->chunk_blocks <= 0 && zbytes <= ((size_t)16 << 30)) {
     HIPCHK(ps->Z.ensure((size_t)pa->n_pol * zr * pa->N * sizeof(float2)));
     float2* Z = ps->Z.as<float2>();
     pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zr * pa->N, z0);
@@ -1055,6 +1063,20 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
 }
 
 // ------------------------------------------------------------------ utilities
+double pfb_calc_output_nbins(int64_t nbins, int32_t channels, int32_t os_nu, int32_t os_de,
+                             int64_t filter_taps, int32_t input_fft_length, int32_t input_overlap) {
+  // calc_output_nbins.m:17-27, in Matlab's double arithmetic
+  const double nu = os_nu, de = os_de, ch = channels;
+  const double step = std::floor(ch * de / nu);
+  const double nblocks_pfb = std::floor(((double)nbins - (double)filter_taps) / step);
+  const double output_pfb = std::floor(step * nblocks_pfb / ch);
+  const double input_keep = (double)input_fft_length - 2.0 * input_overlap;
+  const double nblocks_ipfb = std::floor((output_pfb - 2.0 * input_overlap) / input_keep);
+  const double output_fft_length = (double)input_fft_length * de / nu * ch;  // normalize.m:17
+  const double output_overlap = (double)input_overlap * de / nu * ch;
+  return (output_fft_length - 2.0 * output_overlap) * nblocks_ipfb;
+}
+
 pfb_status pfb_device_malloc(int32_t device, int64_t bytes, void** ptr) {
   if (!ptr || bytes < 0) return fail(PFB_ERR_INVALID_ARG, "bad arguments");
   HIPCHK(hipSetDevice(device));

@@ -9,6 +9,11 @@ namespace pfb {
 
 enum Variant { kBunton = 0, kPadded = 1, kLowCbf = 2 };
 
+// Largest byte extent one raw buffer descriptor may cover: the kernels form 32-bit
+// signed byte offsets from it.  Launchers size their per-workgroup ranges (and plans
+// reject shapes) so that no descriptor needs more; nothing is clamped silently.
+constexpr int64_t kRsrcMaxBytes = 0x7ffffff0;
+
 // Polyphase analysis (polyphase_analysis.m / polyphase_analysis_padded.m).
 struct AnalysisArgs {
   const float2* in;        // [pol][t]

@@ -106,6 +106,8 @@ SYMBOLS = [
                                   c_void_p, c_int64, c_int64, c_void_p]),
     ("pfb_quantize", c_int32, [c_void_p, c_int64, c_int64, c_int32, c_double, c_void_p, c_int64,
                                POINTER(c_double), c_void_p]),
+    ("pfb_calc_output_nbins", c_double, [c_int64, c_int32, c_int32, c_int32, c_int64, c_int32,
+                                         c_int32]),
     ("pfb_last_error", c_char_p, []),
     ("pfb_api_version", c_int32, []),
     ("pfb_device_count", c_int32, []),

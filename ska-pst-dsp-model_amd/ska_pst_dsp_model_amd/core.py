@@ -30,7 +30,7 @@ from .window import PFBWindow, Taper, identity_taper
 __all__ = ["AnalysisPlan", "SynthesisPlan", "polyphase_analysis", "polyphase_analysis_padded",
            "polyphase_analysis_lowcbf",
            "polyphase_synthesis", "analysis_plan", "synthesis_plan", "is_device_array",
-           "roundtrip"]
+           "roundtrip", "calc_output_nbins"]
 
 
 def _torch():
@@ -314,9 +314,10 @@ def roundtrip(analysis: AnalysisPlan, synthesis: SynthesisPlan, x, sample_offset
     through ``pfb_roundtrip_execute`` — the sequence of test_data_pipeline.m:114,132.
 
     Returns ``(chan, out)``: the full channelised product as a (n_pol, K, n_chan)
-    time-major buffer and the (n_pol, n_out) synthesised series.  Bit-identical to
-    ``analysis.execute(x)`` followed by ``synthesis.execute(chan, sample_offset,
-    layout="ptc")``; the library pipelines the two internally (include/pfb_api.h).
+    time-major buffer and the (n_pol, n_out) synthesised series.  ``chan`` is
+    bit-identical to ``analysis.execute(x)``; ``out`` equals ``synthesis.execute(chan,
+    sample_offset, layout="ptc")`` bit for bit on the chunked pipeline and to ~1e-7 on
+    the fused path (include/pfb_api.h, pfb_roundtrip_execute).
     ``chan``/``out`` may be preallocated buffers of the right shapes (graph capture).
     """
     x, dev = analysis._prep_in(x)
@@ -340,6 +341,20 @@ def roundtrip(analysis: AnalysisPlan, synthesis: SynthesisPlan, x, sample_offset
         c_void_p(chan.data_ptr()), K * analysis.n_chan, K, byref(kr), int(sample_offset),
         c_void_p(out.data_ptr()), max(n_out, 1), n_out, byref(no), _stream_of(x)))
     return chan, out
+
+
+# ============================================================================ helpers
+def calc_output_nbins(nbins, channels, os_factor, filter_taps, input_fft_length, input_overlap):
+    """calc_output_nbins.m:1-28 (same arguments: ``os_factor`` a Rational / "nu/de" / Matlab
+    struct-like, ``filter_taps`` the tap COUNT): the number of samples that emerge from
+    channelisation and inversion of ``nbins`` input samples.  Evaluated by the C ABI
+    (``pfb_calc_output_nbins``) in Matlab's double arithmetic; integral results come
+    back as int."""
+    os_ = as_rational(os_factor)
+    v = float(_lib.load().pfb_calc_output_nbins(int(nbins), int(channels), os_.nu, os_.de,
+                                                int(filter_taps), int(input_fft_length),
+                                                int(input_overlap)))
+    return int(v) if v.is_integer() else v
 
 
 # ============================================================================ plan cache

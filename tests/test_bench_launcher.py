@@ -1,0 +1,85 @@
+"""CPU tests of bench.py's multi-GPU entry point (BASELINE C4 sharding).
+
+``bench.py --gpus N`` starts N ranks itself through torch.distributed.run (a child
+process; the parent makes no GPU call), each rank owns its units (one dual-pol DADA
+time block = 2 units, seeds 100+2r, 100+2r+1) and rank 0 reports
+value = all ranks' samples / max-over-ranks time.  Here the device step is stubbed
+(``--stub-device``: a fixed CPU wait, gloo backend), so the launcher, the unit mapping
+and the aggregation run on the CPU.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+
+
+def test_rank_units_cover_c4_seeds_once():
+    seeds = [s for r in range(8) for s in bench.rank_units("c4", r)]
+    assert seeds == list(range(100, 116))  # 16 units, 2 per GPU on 8 GPUs
+    assert bench.rank_units("c2", 0) == [100]
+    assert bench.rank_units("c4", 3) == [106, 107]
+
+
+def test_workload_defaults():
+    class A:
+        workload = "auto"
+    assert bench.resolve_workload(A, 1) == "c2"
+    assert bench.resolve_workload(A, 2) == "c4"
+    A.workload = "c4"
+    assert bench.resolve_workload(A, 1) == "c4"
+
+
+def _run(args, env=None, timeout=240):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, env=e,
+                          capture_output=True, text=True, timeout=timeout, cwd=REPO)
+
+
+def _json_line(stdout):
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_gpus_2_launches_two_ranks_and_aggregates():
+    steps = 4
+    r = _run(["--gpus", "2", "--stub-device", "--steps", str(steps), "--warmup", "1",
+              "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    cfg = d["config"]
+    assert cfg["workload"].startswith("C4")
+    assert cfg["n_pol_per_gpu"] == 2 and cfg["units"] == 4
+    assert cfg["unit_seeds_per_rank"] == [[100, 101], [102, 103]]
+    # value = all ranks' samples / max-over-ranks time
+    samples = 2 * 2 * cfg["n_dat_per_unit"] * steps
+    t = d["ms_per_step"] * steps / 1e3
+    assert abs(d["value"] - samples / t / 1e6) / d["value"] < 1e-3
+    assert d["cpu_baseline"] is None  # the CPU leg runs at N = 1 only
+
+
+def test_gpus_1_is_the_c2_headline():
+    r = _run(["--stub-device", "--steps", "2", "--warmup", "0", "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 1
+    assert d["config"]["workload"].startswith("C2")
+    assert d["config"]["unit_seeds_per_rank"] == [[100]]
+
+
+def test_gpus_must_match_launcher_world():
+    r = _run(["--gpus", "2", "--stub-device", "--no-cpu-baseline"],
+             env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE=1" in (r.stderr + r.stdout)

@@ -1,9 +1,11 @@
 """GPU parity of the HIP kernels (through the C ABI) against the oracle.
 
-Sizes are chosen so the float64 oracle finishes in seconds; full BASELINE sizes are
-covered by size-independent properties in test_gpu_properties.py.
-Tolerance: the reference's np.isclose(atol=1e-6, rtol=1e-6) after dividing both
-sides by the oracle's peak magnitude (conftest.assert_pfb_close).
+Sizes are chosen so the float64 oracle finishes in seconds; the BASELINE C2 size and
+the C3/C4 parameters are compared with the oracle in test_gpu_roundtrip.py, which also
+holds the full-size C3 size-independent properties (impulse position, linearity).
+Tolerance: the reference's np.isclose(atol=1e-6, rtol=1e-6) on unit-amplitude data —
+raw for round trips of unit-amplitude inputs, else both sides divided by the oracle's
+RMS magnitude (conftest.assert_pfb_close, which also reports max / RMS error).
 """
 import numpy as np
 import pytest
@@ -276,7 +278,7 @@ def test_round_trip_test_config(gpu):
     ref = orc.polyphase_synthesis(ref_chan, 1, 128, "8/7",
                                   {"apply_deripple": 1, "filter_coeff": taps}, 1, 16,
                                   orc.pfb_window("tukey", 128, 16))
-    assert_pfb_close(out.cpu().numpy(), ref)
+    assert_pfb_close(out.cpu().numpy(), ref, scale=1.0, what="C1 round trip (raw)")
 
 
 # ----------------------------------------------------------------------------- streaming

@@ -185,6 +185,29 @@ def test_impulse_minus_60dB():
     assert amp[mask].max() <= -60.0 + 20 * np.log10(np.abs(y).max()), amp[mask].max()
 
 
+def test_c3_impulse_delay_and_gain():
+    """SKA-Mid (C3) parameters: an impulse through polyphase_analysis_padded ->
+    polyphase_synthesis comes back with unit gain, <= -60 dB outside +-1 sample
+    (TestImpulse.m:46-73), 458 751 samples early: the output overlap
+    Ov de/nu N = 458 752 minus one (the padded bank's -sds shift centres the (L_h-1)/2
+    group delay, polyphase_analysis_padded.m:89,156; its zero history delays by one
+    block).  The GPU full-size test asserts the same index."""
+    from ska_pst_dsp_model_amd import firio
+    taps = firio.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
+    n, pos = 1 << 22, 40_000_000 % (256 * 3584) + 2 * 256 * 3584
+    x = np.zeros((1, 1, n), np.complex64)
+    x[0, 0, pos] = 1.0
+    ch = orc.polyphase_analysis_padded(x, taps, 4096, "8/7")
+    y = np.abs(orc.polyphase_synthesis(ch, 1, 512, "8/7", {"apply_deripple": 1, "filter_coeff": taps},
+                                       1, 128, orc.pfb_window("tukey", 512, 128))[0, 0])
+    pk = int(np.argmax(y))
+    assert pos - pk == 458751
+    assert abs(y[pk] - 1.0) < 1e-4
+    mask = np.ones(len(y), bool)
+    mask[pk - 1:pk + 2] = False
+    assert 20 * np.log10(y[mask].max()) <= -60.0
+
+
 def test_filterbank_stream_equals_one_shot():
     taps = _design(8, "8/7", 10)
     x = _noise(np.random.default_rng(9), (1, 1, 5000))
