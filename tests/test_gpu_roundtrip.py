@@ -52,6 +52,9 @@ CASES = [
     (512, "8/7", 12, 128, 16, "polyphase_analysis_padded", 1, 1 << 19, 0, 4),
     (1024, "4/3", 12, 256, 48, "polyphase_analysis_padded", 2, 1 << 19, 0, 1),
     (512, "8/7", 12, 128, 16, "polyphase_analysis_padded", 1, 1 << 19, 3, 1),
+    # Nf 512 (4 phases per synthesis workgroup): phase-group-major stage-1 rows
+    (512, "8/7", 12, 512, 128, "polyphase_analysis_padded", 2, 1 << 19, 0, 1),
+    (512, "8/7", 12, 512, 128, "polyphase_analysis", 1, 1 << 19, 0, 3),
     (8, "8/7", 10, 128, 16, "polyphase_analysis", 2, 9000, 1, 1),
     (8, "8/7", 10, 128, 16, "polyphase_analysis_padded", 1, 9000, 2, 3),
 ]
