@@ -102,3 +102,53 @@ def test_verify_metrics_match_util_definitions():
     al = verify.purity_alignment(8, "8/7", 128, 16, 81, 3)
     assert al == {"normalize": 1024, "block_size": 896, "fft_size": 1792, "n_samples": 2688,
                   "output_sample_shift": 112, "total_sample_shift": 152}
+
+
+# ------------------------------------------------------------------ C5 purity scoring
+def test_c5_alignment_constants_mid():
+    """current_performance.m:203-235 + test_data_pipeline.m:136 for sub-config 'mid'
+    (fir_offset_direction 0, kludge_offset 0): the chop offset equals the padded bank's
+    round-trip delay pinned in test_oracle.test_c3_impulse_delay_and_gain (458 751)."""
+    from ska_pst_dsp_model_amd import verify
+    al = verify.performance_alignment(4096, "8/7", 512, 128, 100353, 3, 0, 0)
+    assert al["block_size"] == 1835008 and al["nbins"] == 5505024
+    assert al["additional_offset"] - al["fir_offset"] == 458751
+    assert al["filt_offset"] == 50176 and al["fft_length"] == 3670016
+    items = verify.sweep_vectors(al, 300, 3)
+    t = [p for d, p in items if d == "time"]
+    f = [p for d, p in items if d == "freq"]
+    assert len(f) == 300 and f[0] == 3 and f[1] == 6118 * 3
+    assert t[0] == 1 and 50176 in t and 50176 + 917504 in t
+    # round-robin over 8 GPUs covers every vector exactly once
+    shares = [verify.shard(items, r, 8) for r in range(8)]
+    assert sorted(sum(shares, [])) == sorted(items)
+
+
+def test_c5_scoring_matches_reference_on_oracle():
+    """The C5 scoring (chop.m, DomainPerformance.m, ErrorAnalysis.m) on oracle round
+    trips of the reference's 'low' sub-config (Bunton, 256 ch, 4/3, fir_offset_direction
+    -1, kludge_offset 1): every impulse whose response lies in the output comes back at
+    its aligned index with <= -60 dB outside +-1 sample (TestImpulse.m:46-73), every
+    grid tone has <= -60 dB spurious spectral power (TestPureTone.m:55-89)."""
+    from oracle import pfb_oracle as orc
+    from ska_pst_dsp_model_amd import firio, verify
+    taps = firio.design_PFB_FIR_filter(256, "4/3", 12)
+    al = verify.performance_alignment(256, "4/3", 256, 48, len(taps), 3, -1, 1)
+    win = orc.pfb_window("tukey", 256, 48)
+    items = verify.sweep_vectors(al, 4, 3)
+    scored = 0
+    for kind, p in items:
+        x = verify.time_domain_impulse(al["nbins"], p) if kind == "time" else \
+            verify.complex_sinusoid(al["nbins"], p)
+        ch = orc.polyphase_analysis(x[None, None, :], taps, 256, "4/3")
+        y = orc.polyphase_synthesis(ch, 1, 256, "4/3", {"apply_deripple": 1, "filter_coeff": taps},
+                                    1, 48, win)[0, 0]
+        r = verify.score_vector(kind, p, x, y, al)
+        if kind == "time" and "expected_index" in r:
+            assert r["peak_index"] == r["expected_index"], r
+            assert r["max_outside_pm1_dB"] <= -60.0, r
+            scored += 1
+        elif kind == "freq":
+            assert r["max_spurious_dB"] <= -60.0, r
+            scored += 1
+    assert scored >= 8
