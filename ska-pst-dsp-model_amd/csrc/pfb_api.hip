@@ -523,7 +523,9 @@ struct pfb_synthesis_plan {
   int xcd = 1;       // PFB_SYNTH_XCD=0: plain workgroup order (A/B measurement only)
   bool identity_perm = true;
   bool has_cgain = false;
+  bool has_spectral = false;  // non-identity spectral taper: pfb_spectral.hip path
   DevBuf window, tw4, twN, twNf, twW, perm, cgain;
+  DevBuf taper, gainj, sbuf0, sbuf1;  // spectral taper (L), deripple gains (W), scratch
   DevBuf Z, carry, work, stage_in, stage_out;
   int64_t buffered = 0;
 };
@@ -546,11 +548,60 @@ static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64
                                    int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
                                    hipStream_t s);
 
+// Blocks [b0, b0 + nb) with a spectral taper (pfb_spectral.hip): Matlab's order — per
+// channel FFT, stitch x taper, then the L-point IFFT as row FFTs — in sub-chunks whose
+// scratch stays within 2^26 values per buffer.
+static pfb_status synthesis_spectral(pfb_synthesis_plan* p, const float2* in, int64_t in_ps, int64_t b0,
+                                     int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
+                                     hipStream_t s) {
+  const int64_t per_block = (int64_t)p->N * std::max(p->Nf, p->W);
+  const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(65535, ((int64_t)1 << 26) / per_block));
+  const int64_t nsub = std::min(sub, nb);
+  HIPCHK(p->sbuf0.ensure((size_t)nsub * per_block * sizeof(float2)));
+  HIPCHK(p->sbuf1.ensure((size_t)nsub * per_block * sizeof(float2)));
+  for (int64_t c0 = b0; c0 < b0 + nb; c0 += nsub) {
+    pfb::SpectralArgs a{};
+    a.in = in;
+    a.in_pol_stride = in_ps;
+    a.out = out;
+    a.out_pol_stride = out_ps;
+    a.out_limit = out_limit;
+    a.b0 = c0;
+    a.nb = std::min(nsub, b0 + nb - c0);
+    a.n_pol = p->n_pol;
+    a.N = p->N;
+    a.Nf = p->Nf;
+    a.W = p->W;
+    a.keep = p->keep;
+    a.L = p->L;
+    a.Lov = p->Lov;
+    a.Lkeep = p->Lkeep;
+    a.t1_lo = p->t1_lo;
+    a.t1_hi = p->t1_hi;
+    a.spans = p->spans;
+    a.scale = (float)((double)p->de / (double)p->nu / (double)p->L);
+    a.window = p->window.as<float>();
+    a.cgain = p->has_cgain ? p->cgain.as<float>() : nullptr;
+    a.perm = p->identity_perm ? nullptr : p->perm.as<int>();
+    a.gainj = p->gainj.as<float>();
+    a.taper = p->taper.as<float>();
+    a.twNf = p->twNf.as<float2>();
+    a.twN = p->twN.as<float2>();
+    a.twW = p->twW.as<float2>();
+    a.buf0 = p->sbuf0.as<float2>();
+    a.buf1 = p->sbuf1.as<float2>();
+    ProfScope ps(2, (double)p->n_pol * a.nb * ((double)p->keep * p->N * 8.0 + p->Lkeep * 8.0), s, false);
+    HIPCHK(pfb::launch_spectral_synth(a, s));
+  }
+  return PFB_OK;
+}
+
 // Blocks [b0, b0 + nb) of a call: channel IFFT of their rows into Z, then the block
 // kernel.  `in` is the call's first channelised row (sample_offset applied).
 static pfb_status synthesis_chunk(pfb_synthesis_plan* p, const float2* in, int64_t in_ps, int64_t b0,
                                   int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
                                   hipStream_t s) {
+  if (p->has_spectral) return synthesis_spectral(p, in, in_ps, b0, nb, out, out_ps, out_limit, s);
   const int64_t rows = nb * p->keep + 2 * (int64_t)p->Ov;
   HIPCHK(p->Z.ensure((size_t)p->n_pol * rows * p->N * sizeof(float2)));
   float2* Z = p->Z.as<float2>();
@@ -655,9 +706,20 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
   if (W % 2 != 0) return fail(PFB_ERR_INVALID_ARG, "FN_width %d must be even", W);
   if (d->combine < 1 || N % d->combine != 0)
     return fail(PFB_ERR_INVALID_ARG, "combine=%d must divide n_chan=%d", d->combine, N);
-  if (d->spectral_taper != PFB_WINDOW_NONE)
-    return fail(PFB_ERR_UNSUPPORTED,
-                "non-identity spectral taper is not implemented on the GPU path yet");
+  // spectral tapers act on the stitched L-vector (polyphase_synthesis.m:282): 'hann'
+  // (PFBWindow.m:70-100, circshift(hann(L), L/2) on an L-row column) or explicit L
+  // coefficients; tukey / top_hat index columns 1..Ov of that L x 1 column and have no
+  // defined meaning there
+  if (d->spectral_taper != PFB_WINDOW_NONE && d->spectral_taper != PFB_WINDOW_HANN &&
+      d->spectral_taper != PFB_WINDOW_CUSTOM)
+    return fail(PFB_ERR_INVALID_ARG,
+                "spectral taper %d: only identity, hann or custom (L coefficients) act on the "
+                "stitched spectrum", d->spectral_taper);
+  if (d->spectral_taper == PFB_WINDOW_CUSTOM && !d->spectral_coeffs)
+    return fail(PFB_ERR_INVALID_ARG, "CUSTOM spectral taper without coefficients");
+  if (d->spectral_taper != PFB_WINDOW_NONE &&
+      !pfb::spectral_synth_supported(Nf, (int)(((int64_t)Nf * de) / nu), N))
+    return fail(PFB_ERR_UNSUPPORTED, "no spectral-taper synthesis kernels for Nf=%d n_chan=%d", Nf, N);
   if (!pfb::chan_ifft_supported(N))
     return fail(PFB_ERR_UNSUPPORTED, "no channel-IFFT kernel for n_chan=%d", N);
   if (!pfb::synth_block_supported(Nf, W))
@@ -823,6 +885,23 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
   if (e == hipSuccess) e = upload(p->twN, twiddles(N, -1));
   if (e == hipSuccess) e = upload(p->twNf, twiddles(Nf, -1));
   if (e == hipSuccess) e = upload(p->twW, twiddles(W, -1));
+  if (e == hipSuccess && d->spectral_taper != PFB_WINDOW_NONE) {
+    p->has_spectral = true;
+    std::vector<float> taper((size_t)p->L);
+    if (d->spectral_taper == PFB_WINDOW_HANN) {
+      // hann(L) circularly shifted by L/2 (PFBWindow.m:83-95: ndat = L != Nf)
+      std::vector<double> h;
+      hann_sym(p->L, h);
+      for (int i = 0; i < p->L; ++i) taper[(size_t)i] = (float)h[(size_t)((i - p->L / 2 + p->L) % p->L)];
+    } else {
+      for (int i = 0; i < p->L; ++i) taper[(size_t)i] = (float)d->spectral_coeffs[i];
+    }
+    // deripple gains in Matlab's FN row order j (polyphase_synthesis.m:244-250)
+    std::vector<float> gj((size_t)W);
+    for (int j = 0; j < W; ++j) gj[(size_t)j] = (float)((j < W2) ? g[(size_t)(W2 - j)] : g[(size_t)(j - W2)]);
+    e = upload(p->taper, taper);
+    if (e == hipSuccess) e = upload(p->gainj, gj);
+  }
   if (e != hipSuccess) {
     delete p;
     return fail(PFB_ERR_HIP, "synthesis plan upload: %s", hipGetErrorString(e));
@@ -834,8 +913,9 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
 pfb_status pfb_synthesis_plan_destroy(pfb_synthesis_plan* p) {
   if (!p) return PFB_OK;
   (void)hipSetDevice(p->device);
-  for (DevBuf* b : {&p->window, &p->tw4, &p->twN, &p->twNf, &p->twW,
-                    &p->perm, &p->cgain, &p->Z, &p->carry, &p->work, &p->stage_in, &p->stage_out})
+  for (DevBuf* b : {&p->window, &p->tw4, &p->twN, &p->twNf, &p->twW, &p->perm, &p->cgain,
+                    &p->taper, &p->gainj, &p->sbuf0, &p->sbuf1, &p->Z, &p->carry, &p->work,
+                    &p->stage_in, &p->stage_out})
     b->release();
   delete p;
   return PFB_OK;
@@ -1016,7 +1096,7 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
   const int64_t z0 = pa->fused ? off : 0;
   const int64_t zr = K - z0;
   const size_t zbytes = (size_t)pa->n_pol * zr * pa->N * sizeof(float2);
-  if (!no_fuse && analysis_emits_z(pa) && ps->identity_perm && !ps->has_cgain &&
+  if (!no_fuse && analysis_emits_z(pa) && ps->identity_perm && !ps->has_cgain && !ps->has_spectral &&
       ps->chunk_blocks <= 0 && zbytes <= ((size_t)16 << 30)) {
     HIPCHK(ps->Z.ensure((size_t)pa->n_pol * zr * pa->N * sizeof(float2)));
     float2* Z = ps->Z.as<float2>();

@@ -87,6 +87,32 @@ struct SynthBlockArgs {
                            // bit1 drop output stores, bit2 drop tw4 loads (results invalid)
 };
 
+// Synthesis with a non-identity spectral taper (pfb_spectral.hip): blocks [b0, b0 + nb)
+// of the call, every polarisation, through two scratch buffers of nb N max(Nf, W) values.
+struct SpectralArgs {
+  const float2* in;        // [pol][row][c] channelised rows of the call (sample offset applied)
+  int64_t in_pol_stride;
+  float2* out;             // [pol][t]
+  int64_t out_pol_stride;
+  int64_t out_limit;
+  int64_t b0, nb;
+  int n_pol;
+  int N, Nf, W, keep, L, Lov, Lkeep, t1_lo, t1_hi, spans;
+  float scale;             // (de/nu) / L
+  const float* window;     // Nf temporal window
+  const float* cgain;      // per input channel gain (temporal 'hann' quirk) or null
+  const int* perm;         // combine permutation (slot -> input channel) or null
+  const float* gainj;      // W deripple gains in Matlab's FN row order
+  const float* taper;      // L spectral taper coefficients
+  const float2* twNf;      // e^{-2 pi i m / Nf}
+  const float2* twN;       // e^{-2 pi i m / N}
+  const float2* twW;       // e^{-2 pi i m / W}
+  float2* buf0;
+  float2* buf1;
+};
+bool spectral_synth_supported(int Nf, int W, int N);
+hipError_t launch_spectral_synth(const SpectralArgs& a, hipStream_t s);
+
 // SKA-Low CBF PST filterbank (polyphase_analysis_lowcbf.m / PSTFilterbank.m):
 // 256 arms x 12 taps, step 192, forward FFT, fftshift, pi/2 derotation, 216 channels.
 struct LowCbfArgs {

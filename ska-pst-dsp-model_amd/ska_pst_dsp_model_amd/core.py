@@ -161,12 +161,22 @@ class AnalysisPlan:
 
 
 # ============================================================================ synthesis
-def _resolve_taper(taper, nf: int, ov: int):
-    """Translate a taper handle into (kind, coeffs) for the C ABI."""
+def _resolve_taper(taper, nf: int, ov: int, spectral_length: int = 0):
+    """Translate a taper handle into (kind, coeffs) for the C ABI.  ``spectral_length``
+    > 0: the handle is a SPECTRAL taper over the L = spectral_length stitched bins
+    (polyphase_synthesis.m:282); custom coefficients must then number L."""
     if taper is None or taper is identity_taper:
         return _lib.PFB_WINDOW_NONE, None
     if isinstance(taper, str):
         taper = PFBWindow().lookup[taper](nf, ov)
+    if isinstance(taper, Taper) and spectral_length:
+        if taper.kind == _lib.PFB_WINDOW_CUSTOM:
+            c = np.asarray(taper.coeffs, dtype=np.float64).ravel()
+            if c.size != spectral_length:
+                raise ValueError(f"custom spectral taper needs {spectral_length} coefficients, "
+                                 f"got {c.size}")
+            return taper.kind, c
+        return taper.kind, None  # hann: the plan builds circshift(hann(L), L/2)
     if isinstance(taper, Taper):
         if taper.kind == _lib.PFB_WINDOW_CUSTOM:
             return taper.kind, np.asarray(taper.coeffs, dtype=np.float64)
@@ -212,7 +222,8 @@ class SynthesisPlan:
         self.device = int(device)
         nf, ov = self.input_fft_length, self.input_overlap
         tk, tco = _resolve_taper(temporal_taper, nf, ov)
-        sk, sco = _resolve_taper(spectral_taper, nf, ov)
+        L = (nf * self.os_factor.de // self.os_factor.nu) * self.n_chan
+        sk, sco = _resolve_taper(spectral_taper, nf, ov, spectral_length=L)
         taps = _taps64(filter_coeff) if filter_coeff is not None else np.zeros(1)
         self._keep = []
         tarr, tptr = _lib.c_double_array(taps)
@@ -386,7 +397,7 @@ def synthesis_plan(n_chan, os_factor, nf, ov, spans, combine, deripple, filt, t_
                    n_pol, device=0) -> SynthesisPlan:
     os_ = as_rational(os_factor)
     tk, tco = _resolve_taper(t_taper, nf, ov)
-    sk, sco = _resolve_taper(s_taper, nf, ov)
+    sk, sco = _resolve_taper(s_taper, nf, ov, spectral_length=(nf * os_.de // os_.nu) * int(n_chan))
     taps = _taps64(filt) if (deripple and filt is not None) else None
     k = _key("s", int(n_chan), str(os_), int(nf), int(ov), bool(spans), int(combine),
              bool(deripple), taps if taps is not None else "-", tk,

@@ -394,3 +394,24 @@ def test_purity_sweep_ska_mid(gpu):
     assert comb["comb_test"] == 0, comb
     sq = [r for r in recs if r["domain"] == "square_wave"][0]
     assert 0.9 < sq["on_power"] < 1.1 and sq["off_power"] < 1e-3, sq
+
+
+def test_two_stage_inverse_frequency_taper(gpu):
+    """TwoStageInverseFilterBank.frequency_taper('hann') (TwoStageInverseFilterBank.m:57-70)
+    on the critical / combine-2 inversion (stage-2 banks of 28 channels)."""
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(16, "8/7", 10)
+    cfg = dict(filt_coeff=taps, channels=16, os_factor="8/7", input_fft_length=128,
+               input_overlap=16, deripple=False, temporal_taper="tukey")
+    ti = pfb.TwoStageInverseFilterBank(cfg)
+    ti.nch2 = 14
+    ti.combine = 2
+    ti.frequency_taper("hann")
+    oti = orc.TwoStageInverseFilterBankOracle(
+        lambda: orc.InverseFilterBankOracle(taps, 16, "8/7", 128, 16, "tukey").frequency_taper("hann"),
+        14, combine=2)
+    rng = np.random.default_rng(23)
+    x = _noise(rng, (1, 4 * 14, 700))
+    ti, got = ti.execute(x)
+    ref = oti.execute(x)
+    assert_pfb_close(got, ref, what="two-stage inverse, hann spectral taper")

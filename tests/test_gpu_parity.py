@@ -334,3 +334,82 @@ def test_inverse_filterbank_streaming_matches_oracle(gpu):
         if ref.size:
             assert_pfb_close(got, ref)
         assert ifb.buffered_samples == oifb.buffered_samples
+
+
+# ----------------------------------------------------------------------------- spectral taper
+# polyphase_synthesis.m:282 (FFFF = spectral_taper(FFFF, L, Ov)) through
+# InverseFilterBank.frequency_taper (InverseFilterBank.m:48-61); 'hann' on the L-vector
+# is circshift(hann(L), L/2) (PFBWindow.m:83-95).  GPU path: pfb_spectral.hip.
+@pytest.mark.parametrize("spans", [1, 0])
+@pytest.mark.parametrize("deripple", [1, 0])
+def test_synthesis_spectral_hann_matches_oracle(gpu, spans, deripple):
+    import torch
+    pfb = _pfb()
+    taps = _taps("test")
+    x = _noise(np.random.default_rng(51), (2, 8, 96 * 5 + 32 + 3))
+    dr = {"apply_deripple": deripple, "filter_coeff": taps}
+    ref = orc.polyphase_synthesis(x, spans, 128, "8/7", dr, 1, 16, orc.pfb_window("tukey", 128, 16),
+                                  orc.pfb_window("hann", 128, 16))
+    w = pfb.PFBWindow()
+    got = pfb.polyphase_synthesis(torch.from_numpy(x).to(gpu), spans, 128, "8/7", dr, 1, 16,
+                                  w.lookup["tukey"](128, 16), w.lookup["hann"](128, 16))
+    assert_pfb_close(got.cpu().numpy(), ref, what=f"spectral hann spans={spans} dr={deripple}")
+
+
+def test_synthesis_spectral_hann_c2prime(gpu):
+    """C2' shape (SKA-Low 256 ch, 4/3, Nf 256, Ov 48, deripple) with the hann spectral taper."""
+    import torch
+    pfb = _pfb()
+    taps = _taps("low43")
+    x = _noise(np.random.default_rng(52), (1, 256, 160 * 6 + 96 + 7))
+    dr = {"apply_deripple": 1, "filter_coeff": taps}
+    ref = orc.polyphase_synthesis(x, 1, 256, "4/3", dr, 1, 48, orc.pfb_window("tukey", 256, 48),
+                                  orc.pfb_window("hann", 256, 48))
+    w = pfb.PFBWindow()
+    got = pfb.polyphase_synthesis(torch.from_numpy(x).to(gpu), 1, 256, "4/3", dr, 1, 48,
+                                  w.lookup["tukey"](256, 48), w.lookup["hann"](256, 48))
+    assert_pfb_close(got.cpu().numpy(), ref, what="C2' spectral hann")
+
+
+def test_synthesis_spectral_custom_and_combine(gpu):
+    """Explicit L spectral coefficients (API extension), critical + combine 2."""
+    import torch
+    pfb = _pfb()
+    taps = _taps("test")
+    L = 112 * 8
+    coeffs = np.random.default_rng(53).uniform(0.2, 1.0, L)
+    x = _noise(np.random.default_rng(54), (1, 8, 96 * 4 + 32))
+
+    def taper(a, *args):
+        return coeffs[:, None] * a
+
+    ref = orc.polyphase_synthesis(x, 0, 128, "8/7", None, 1, 16, orc.pfb_window("tukey", 128, 16),
+                                  taper, 2)
+    w = pfb.PFBWindow()
+    got = pfb.polyphase_synthesis(torch.from_numpy(x).to(gpu), 0, 128, "8/7", None, 1, 16,
+                                  w.lookup["tukey"](128, 16), w.custom(coeffs), 2)
+    assert_pfb_close(got.cpu().numpy(), ref, what="custom spectral taper, combine 2")
+    with pytest.raises(ValueError):
+        pfb.polyphase_synthesis(torch.from_numpy(x).to(gpu), 0, 128, "8/7", None, 1, 16,
+                                None, w.custom(coeffs[:100]))
+    with pytest.raises(pfb.PfbError):  # tukey has no meaning on the L-vector
+        pfb.polyphase_synthesis(torch.from_numpy(x).to(gpu), 0, 128, "8/7", None, 1, 16,
+                                None, w.lookup["tukey"](128, 16))
+
+
+def test_inverse_filterbank_frequency_taper_stream(gpu):
+    """InverseFilterBank.frequency_taper('hann') (InverseFilterBank.m:48-61) streaming."""
+    pfb = _pfb()
+    taps = _taps("test")
+    cfg = dict(filt_coeff=taps, channels=8, os_factor="8/7", input_fft_length=128,
+               input_overlap=16, deripple=False, temporal_taper="tukey")
+    ifb = pfb.InverseFilterBank(cfg).frequency_taper("hann")
+    oifb = orc.InverseFilterBankOracle(taps, 8, "8/7", 128, 16, "tukey").frequency_taper("hann")
+    rng = np.random.default_rng(55)
+    for n in (500, 333, 1000):
+        x = _noise(rng, (2, 8, n))
+        ifb, got = ifb.execute(x)
+        ref = oifb.execute(x)
+        assert got.shape == ref.shape
+        if ref.size:
+            assert_pfb_close(got, ref, what=f"inverse filterbank hann n={n}")
