@@ -1,6 +1,6 @@
 #!/bin/bash
-# C3 (SKA-Mid) A/B: round-trip tests, then bench_aux --only-mid with and without the
-# phase-group-major stage-1 rows, then a kernel trace of the C3 round trip.
+# C3 (SKA-Mid) A/B: round-trip tests, then bench_aux --only-mid with the default and an
+# alternative environment (AB_ENV), then a kernel trace of the C3 round trip.
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -12,8 +12,8 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 for i in 1 2; do
   timeout -k 10 200 python scripts/bench_aux.py --only-mid --reps 10 > gpurun_out/c3_new_$i.jsonl 2> gpurun_out/c3.err || exit $?
   cat gpurun_out/c3_new_$i.jsonl
-  PFB_RT_NO_ZGROUP=1 timeout -k 10 200 python scripts/bench_aux.py --only-mid --reps 10 > gpurun_out/c3_old_$i.jsonl 2> gpurun_out/c3.err || exit $?
-  echo "old:"; cat gpurun_out/c3_old_$i.jsonl
+  env ${AB_ENV:-PFB_NONE=1} timeout -k 10 200 python scripts/bench_aux.py --only-mid --reps 10 > gpurun_out/c3_old_$i.jsonl 2> gpurun_out/c3.err || exit $?
+  echo "alt (${AB_ENV:-}):"; cat gpurun_out/c3_old_$i.jsonl
 done
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/c3prof -o run \
     -- python3 $R/scripts/bench_aux.py --only-mid --reps 5 > $R/gpurun_out/c3prof.log 2>&1 || exit $?

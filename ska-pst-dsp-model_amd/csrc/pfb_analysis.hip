@@ -116,7 +116,7 @@ __global__ __launch_bounds__(NT) void analysis_fused_kernel(AnalysisArgs a) {
   // twiddle table -> LDS, behind the FFT rows (the staged span is dead after the FIR)
   const float2 twv = a.twN[tid & (N - 1)];
   __syncthreads();
-  if (tid < N) smem[T * S_::RS + tid] = twv;
+  if (tid < N) smem[T * S_::RS + tw_slot(tid)] = twv;
 
   // 4. circular shift folded into the LDS write address
   //    Bunton: v[(n + r) mod N] = u[n], r = (M k) mod N               (polyphase_analysis.m:102-105)
@@ -174,7 +174,7 @@ struct StreamShape {
   static constexpr int WIN = NEW + PE - 1;  // register window (rows)
   static constexpr int RS = lds_row(N);
   static constexpr int TW_OFF = T * RS;               // float2 offset of the twiddles
-  static constexpr int F_OFF = 2 * (TW_OFF + N);      // float offset of the taps F
+  static constexpr int F_OFF = 2 * (TW_OFF + tw_slots(N));  // float offset of the taps F
   static constexpr int F_LEN = (P + 2) * N;
   static constexpr size_t lds_bytes = (size_t)F_OFF * sizeof(float) + F_LEN * sizeof(float);
 };
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
 
   // LDS: twiddles behind the FFT rows, then F = [N zeros, taps, zeros]
   float* F = reinterpret_cast<float*>(smem) + SH::F_OFF;
-  smem[SH::TW_OFF + c] = a.twN[c];
+  smem[SH::TW_OFF + tw_slot(c)] = a.twN[c];
 #pragma unroll
   for (int m = 0; m < P + 2; ++m) F[m * N + c] = (m >= 1 && m <= P) ? a.taps[(m - 1) * N + c] : 0.f;
 
@@ -552,7 +552,7 @@ template <int N, int PMAX, int VARIANT, int TDIV, bool EXACT = false>
 static hipError_t launch_fused(const AnalysisArgs& a, hipStream_t s) {
   using S_ = AnaShape<N, PMAX, TDIV>;
   const size_t span = (size_t)a.M * (S_::T - 1) + (size_t)a.P * N;
-  const size_t rows = (size_t)S_::T * S_::RS + N;  // FFT rows + twiddle table
+  const size_t rows = (size_t)S_::T * S_::RS + tw_slots(N);  // FFT rows + twiddle table
   const size_t bytes = ((span + 1 > rows) ? span + 1 : rows) * sizeof(float2);
   auto kern = analysis_fused_kernel<N, PMAX, VARIANT, TDIV, EXACT>;
   hipError_t e = set_lds(kern, bytes);

@@ -156,7 +156,7 @@ __global__ __launch_bounds__(NT) void row_fft_kernel(RowFftArgs a) {
   }
 #pragma unroll
   for (int i = 0; i < TPT; ++i)
-    if (threadIdx.x + i * NT < N) tw[threadIdx.x + i * NT] = twv[i];
+    if (threadIdx.x + i * NT < N) tw[tw_slot(threadIdx.x + i * NT)] = twv[i];
   block_fft<N, DIR, ROWS, NT>(ld, st, rows, tw, threadIdx.x);
 }
 

@@ -249,10 +249,17 @@ struct LdsIO {
   __device__ __forceinline__ void store(int row, int i, float2 v) const { base[row * rs + lpad(i)] = v; }
 };
 
-// Twiddle e^{DIR 2 pi i m / N} from a table tw[m] = e^{-2 pi i m / N} (N entries).
+// LDS twiddle tables are padded by one slot every 32 entries: the power-of-two strided
+// reads of twiddle_powers (index r m, m = k N / (NS R)) otherwise land on a few banks
+// (e.g. m = 16 k: every even k on one bank).  Entry m sits at tw_slot(m); a table of n
+// entries occupies tw_slots(n) float2 slots (even, so what follows stays 16-B aligned).
+__host__ __device__ constexpr int tw_slot(int m) { return m + (m >> 5); }
+__host__ __device__ constexpr int tw_slots(int n) { return (n + (n >> 5) + 2) & ~1; }
+
+// Twiddle e^{DIR 2 pi i m / N} from a padded LDS table, entry m = e^{-2 pi i m / N}.
 template <int DIR>
 __device__ __forceinline__ float2 table_tw(const float2* __restrict__ tw, int m) {
-  float2 w = tw[m];
+  float2 w = tw[tw_slot(m)];
   if constexpr (DIR > 0) w.y = -w.y;
   return w;
 }

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(NT) void lowcbf_kernel(LowCbfArgs a) {
   for (int m = 0; m < LP; ++m) f[m] = a.taps[n + LN * m];
   LdsRows rows(smem, RS);
   float2* tw = smem + LROWS * RS;
-  tw[n] = a.tw[n];
+  tw[tw_slot(n)] = a.tw[n];
   const bool interior = k0 * LM - a.pad >= 0 &&
                         (k0 + LROWS - 1) * LM + LN * LP - a.pad <= a.n_dat && k0 + LROWS <= a.K;
   if (interior) {
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(NT) void lowcbf_kernel(LowCbfArgs a) {
 hipError_t launch_lowcbf(const LowCbfArgs& a, hipStream_t s) {
   if (a.K <= 0) return hipSuccess;
   static_assert(NT == LN, "one thread per polyphase arm");
-  const size_t bytes = ((size_t)LROWS * lds_row(LN) + LN) * sizeof(float2);
+  const size_t bytes = ((size_t)LROWS * lds_row(LN) + tw_slots(LN)) * sizeof(float2);
   hipError_t e = set_lds(lowcbf_kernel, bytes);
   if (e != hipSuccess) return e;
   dim3 grid((unsigned)((a.K + LROWS - 1) / LROWS), (unsigned)a.n_pol);

@@ -8,7 +8,7 @@ namespace pfb {
 template <int N, int DIR, bool PERM, bool GAIN>
 static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s) {
   constexpr int ROWS = RowShape<N>::ROWS;
-  const size_t bytes = ((size_t)ROWS * RowShape<N>::RS + N) * sizeof(float2);
+  const size_t bytes = ((size_t)ROWS * RowShape<N>::RS + tw_slots(N)) * sizeof(float2);
   auto kern = row_fft_kernel<N, DIR, PERM, GAIN>;
   hipError_t e = set_lds(kern, bytes);
   if (e != hipSuccess) return e;

@@ -128,7 +128,7 @@ __global__ __launch_bounds__(NT) void w_out_kernel(WOutLoad ld, WOutStore st, co
   s.r0 = r0;
   LdsRows rows(smem, RowShape<W>::RS);
   float2* tw = smem + ROWS * RowShape<W>::RS;
-  for (int i = threadIdx.x; i < W; i += NT) tw[i] = twW[i];
+  for (int i = threadIdx.x; i < W; i += NT) tw[tw_slot(i)] = twW[i];
   __syncthreads();
   block_fft<W, +1, ROWS, NT>(l, s, rows, tw, threadIdx.x);
 }
@@ -137,7 +137,7 @@ template <int W>
 static hipError_t launch_w_out(const WOutLoad& l, const WOutStore& s, const float2* twW, int64_t rows,
                                hipStream_t st) {
   constexpr int ROWS = RowShape<W>::ROWS;
-  const size_t bytes = ((size_t)ROWS * RowShape<W>::RS + W) * sizeof(float2);
+  const size_t bytes = ((size_t)ROWS * RowShape<W>::RS + tw_slots(W)) * sizeof(float2);
   auto kern = w_out_kernel<W>;
   hipError_t e = set_lds(kern, bytes);
   if (e != hipSuccess) return e;

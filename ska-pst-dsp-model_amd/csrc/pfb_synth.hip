@@ -23,13 +23,16 @@ constexpr int NTP = 128;  // threads per synthesis workgroup
 
 template <int NF, int W, int PAIRS>
 struct SynthPairShape {
-  // pair-row strides (16-byte slots): N + 7 minimises ds_read/write_b128 bank
-  // conflicts of the radix-16 passes (scripts/lds_bank_sim.py)
-  static constexpr int RSF = NF + 7;
-  static constexpr int RSW = W + 7;
+  // pair-row strides (16-byte slots): N + 7 minimises ds_read/write_b128 bank conflicts
+  // of the radix-16 passes of the SKA-Low shapes; the SKA-Mid plan (Nf 512 = 8 x 4 x 16,
+  // W 448 = 14 x 8 x 4, 4 pair rows) is conflict-free except its fused reads with
+  // Nf + 2 / W + 4 (LDS bank model over every pass's lane groups)
+  static constexpr int RSF = NF + (NF == 512 ? 2 : 7);
+  static constexpr int RSW = W + (W == 448 ? 4 : 7);
   static constexpr int RSMAX = RSF > RSW ? RSF : RSW;
   static constexpr int TWOFF = PAIRS * RSMAX * 2;  // float2 offset of the twiddle tables
-  static constexpr size_t lds_bytes = (size_t)(TWOFF + NF + W) * sizeof(float2) + NF * sizeof(float);
+  static constexpr size_t lds_bytes =
+      (size_t)(TWOFF + tw_slots(NF) + tw_slots(W)) * sizeof(float2) + NF * sizeof(float);
 };
 
 template <int NF, int W, bool SPANS>
@@ -253,8 +256,8 @@ __device__ __forceinline__ void fused_select_pass(const LdsPairs& rowsF, const L
 // and read from there every block (SKA-Mid: the 14.7 MB table was re-read from L2/MALL
 // for each of a workgroup's blocks; only where the copy keeps 4 workgroups per CU).
 template <int NF, int W, int PAIRS, bool SPANS, bool PERSIST, int DK = 0, bool P16 = false,
-          bool T4L = false>
-__global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void synth_block_kernel(SynthBlockArgs a) {
+          bool T4L = false, int NTPW = NTP>
+__global__ __launch_bounds__(NTPW) __attribute__((amdgpu_waves_per_eu(2))) void synth_block_kernel(SynthBlockArgs a) {
   using SS = SynthPairShape<NF, W, PAIRS>;
   using SP = SynthPlan<NF, W>;
   constexpr int R1 = synth_first_radix<NF, W>();
@@ -279,11 +282,14 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
   const int t0 = tg * TG;
   const int pol = blockIdx.y;
 
-  float2* twF = smem + SS::TWOFF;  // Nf twiddles, then W twiddles, then the taper
-  float2* twWl = twF + NF;
-  float* win = reinterpret_cast<float*>(twWl + W);
-  for (int j = tid; j < NF + W; j += NTP) twF[j] = (j < NF) ? a.twNf[j] : a.twW[j - NF];
-  for (int j = tid; j < NF; j += NTP) win[j] = a.window[j];
+  float2* twF = smem + SS::TWOFF;  // Nf twiddles, then W twiddles (padded), then the taper
+  float2* twWl = twF + tw_slots(NF);
+  float* win = reinterpret_cast<float*>(twWl + tw_slots(W));
+  for (int j = tid; j < NF + W; j += NTPW) {
+    if (j < NF) twF[tw_slot(j)] = a.twNf[j];
+    else twWl[tw_slot(j - NF)] = a.twW[j - NF];
+  }
+  for (int j = tid; j < NF; j += NTPW) win[j] = a.window[j];
 
   const float2* zpol = a.Z + pol * a.z_pol_stride + t0;
   const uint32_t zbytes = (a.timing_mask & 1) ? 0u : (uint32_t)((NF - 1) * N + TG) * 8u;
@@ -291,7 +297,7 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
   const __amdgpu_buffer_rsrc_t tw4r = make_rsrc(a.tw4 + t0, twbytes);
   v4f* t4l = reinterpret_cast<v4f*>(reinterpret_cast<char*>(smem) + SS::lds_bytes);
   if constexpr (T4L) {
-    for (int i = tid; i < W * PAIRS; i += NTP) {
+    for (int i = tid; i < W * PAIRS; i += NTPW) {
       const int jr = i / PAIRS, q = i % PAIRS;
       t4l[i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(tw4r, (jr * N + 2 * q) * 8, 0, 0));
     }
@@ -317,30 +323,30 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
     const int b = b_begin;
     const PairZIn<NB1> in{make_rsrc(zpol + (int64_t)b * a.keep * N, zbytes), N, win};
     const PairSelect<NF, W, SPANS> sel{rowsW, tw4r, N};
-    block_fft_pair<NF, -1, PAIRS, NTP>(in, sel, rowsF, twF, tid);
+    block_fft_pair<NF, -1, PAIRS, NTPW>(in, sel, rowsF, twF, tid);
     __syncthreads();
-    block_fft_pair<W, +1, PAIRS, NTP>(rowsW, out_for(b), rowsW, twWl, tid);
+    block_fft_pair<W, +1, PAIRS, NTPW>(rowsW, out_for(b), rowsW, twWl, tid);
   } else {
     constexpr int NBL = NF / SP::RL;
     constexpr int RW1 = W / NBL;
-    constexpr int PT = (PAIRS * NBL + NTP - 1) / NTP;
+    constexpr int PT = (PAIRS * NBL + NTPW - 1) / NTPW;
     // Nf passes 1 .. last-1 (the first from `in`), then the fused pass, then W passes 2..
     auto run_block = [&](const auto& in, int b, auto after_first) {
-      stockham_pass_pair<NF, R1, 1, -1, PAIRS, NTP>(in, rowsF, twF, tid);
+      stockham_pass_pair<NF, R1, 1, -1, PAIRS, NTPW>(in, rowsF, twF, tid);
       // the gain x twiddle loads go out BEFORE the next block's prefetch: vmcnt retires
       // in order, so waiting for them must not mean waiting for the HBM prefetch too
       v4f t4[PT][RW1];
-      if constexpr (T4L) load_t4_lds<NBL, RW1, PAIRS, NTP>(t4, t4l, tid);
-      else load_t4<NBL, RW1, PAIRS, NTP>(t4, tw4r, N, tid);
+      if constexpr (T4L) load_t4_lds<NBL, RW1, PAIRS, NTPW>(t4, t4l, tid);
+      else load_t4<NBL, RW1, PAIRS, NTPW>(t4, tw4r, N, tid);
       after_first();
       __syncthreads();
       if constexpr (!std::is_same_v<typename SP::Mid, Radices<>>) {
-        run_fft_mid<NF, -1, PAIRS, NTP, R1>(rowsF, twF, tid, typename SP::Mid{});
+        run_fft_mid<NF, -1, PAIRS, NTPW, R1>(rowsF, twF, tid, typename SP::Mid{});
         __syncthreads();
       }
-      fused_select_pass<NF, W, SP::RL, SPANS, PAIRS, NTP>(rowsF, rowsW, twF, t4, tid);
+      fused_select_pass<NF, W, SP::RL, SPANS, PAIRS, NTPW>(rowsF, rowsW, twF, t4, tid);
       __syncthreads();
-      run_fft_tail<W, +1, PAIRS, NTP, RW1>(rowsW, out_for(b), twWl, tid, typename SP::Wrest{});
+      run_fft_tail<W, +1, PAIRS, NTPW, RW1>(rowsW, out_for(b), twWl, tid, typename SP::Wrest{});
     };
     if constexpr (!PERSIST) {
       __syncthreads();  // tables
@@ -348,14 +354,14 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
       const PairZIn<NB1> in{make_rsrc(zpol + (int64_t)b * a.keep * N, zbytes), N, win};
       run_block(in, b, [] {});
     } else {
-      constexpr int PF = (PAIRS * NB1 + NTP - 1) / NTP;
+      constexpr int PF = (PAIRS * NB1 + NTPW - 1) / NTPW;
       v4f zv[PF][R1];
       static_assert(DK >= 0 && DK <= R1, "overlap reuse needs keep = DK * NF / R1");
       auto prefetch = [&](int b, auto reuse) {
         constexpr int R0 = decltype(reuse)::value ? R1 - DK : 0;  // registers kept
         const __amdgpu_buffer_rsrc_t z = make_rsrc(zpol + (int64_t)b * a.keep * N, zbytes);
         static_for<0, PF>([&](auto p) {
-          const int bb = min(tid + p * NTP, PAIRS * NB1 - 1);
+          const int bb = min(tid + p * NTPW, PAIRS * NB1 - 1);
           const int q = bb % PAIRS, j = bb / PAIRS;
           static_for<0, R0>([&](auto r) { zv[p][r] = zv[p][r + DK]; });
           static_for<R0, R1>([&](auto r) {
@@ -380,10 +386,12 @@ __global__ __launch_bounds__(NTP) __attribute__((amdgpu_waves_per_eu(2))) void s
   }
 }
 
-template <int NF, int W, int PAIRS, bool SPANS>
+template <int NF, int W, int PAIRS, bool SPANS, int NTPW = NTP>
 static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
   using SS = SynthPairShape<NF, W, PAIRS>;
   const int groups = a.N / (2 * PAIRS);
+  // workgroups per CU the registers allow at the kernel's 2 waves per SIMD
+  constexpr int vgpr_wgs = 8 * 64 / NTPW;
   if (a.ranges != 0 && SynthPlan<NF, W>::fused) {
     // persistent: block ranges so that ~LDS-limited workgroups per CU are resident;
     // the overlap-reuse instance when keep matches the compiled DK
@@ -395,18 +403,18 @@ static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
     // table copy in LDS where it still leaves 4 two-wave workgroups per CU (the VGPR
     // limit): SKA-Mid 25.7 + 14 KB; not SKA-Low (38.5 + 28 KB)
     constexpr size_t t4_bytes = (size_t)W * PAIRS * 16;
-    constexpr bool T4 = SS::lds_bytes + t4_bytes <= (160 * 1024) / 4;
+    constexpr bool T4 = SS::lds_bytes + t4_bytes <= (160 * 1024) / vgpr_wgs;
     static const bool no_t4l = std::getenv("PFB_SYNTH_NO_T4LDS") != nullptr;
     const bool t4l = T4 && !no_t4l && reuse && p16;
     const size_t lds = SS::lds_bytes + (t4l ? t4_bytes : 0);
-    auto kern = t4l ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true, T4>
-              : reuse ? (p16 ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true>
-                             : synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, false>)
-                      : (p16 ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, 0, true>
-                             : synth_block_kernel<NF, W, PAIRS, SPANS, FU, 0, false>);
+    auto kern = t4l ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true, T4, NTPW>
+              : reuse ? (p16 ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true, false, NTPW>
+                             : synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, false, false, NTPW>)
+                      : (p16 ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, 0, true, false, NTPW>
+                             : synth_block_kernel<NF, W, PAIRS, SPANS, FU, 0, false, false, NTPW>);
     hipError_t e = set_lds(kern, lds);
     if (e != hipSuccess) return e;
-    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / lds));
+    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(vgpr_wgs, (160 * 1024) / lds));
     // resident-capacity ranges; when that leaves more than 16 blocks per range (many
     // phase groups per block row: SKA-Mid N / TG = 1024 gives one range of 72 blocks),
     // ranges of 6 blocks instead (oversubscribed, evenly split): C3 1.59 -> 1.51 ms.
@@ -418,19 +426,27 @@ static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
     }
     ranges = std::min(ranges, a.n_blocks);
     dim3 grid((unsigned)(groups * ranges), (unsigned)a.n_pol);
-    return launch_kernel(kern, grid, dim3(NTP), lds, s, a);
+    return launch_kernel(kern, grid, dim3(NTPW), lds, s, a);
   }
-  auto kern = synth_block_kernel<NF, W, PAIRS, SPANS, false>;
+  auto kern = synth_block_kernel<NF, W, PAIRS, SPANS, false, 0, false, false, NTPW>;
   hipError_t e = set_lds(kern, SS::lds_bytes);
   if (e != hipSuccess) return e;
   dim3 grid((unsigned)(groups * a.n_blocks), (unsigned)a.n_pol);
-  return launch_kernel(kern, grid, dim3(NTP), SS::lds_bytes, s, a);
+  return launch_kernel(kern, grid, dim3(NTPW), SS::lds_bytes, s, a);
 }
 
 // pair rows per workgroup: enough for every thread to own one first-pass butterfly,
 // fewer when the channel count is small (2 * PAIRS must divide N)
 template <int NF, int W, bool SPANS>
 static hipError_t launch_sb_p(const SynthBlockArgs& a, hipStream_t s) {
+  // Nf >= 512 (SKA-Mid): 256-thread workgroups, so one workgroup reads 8 output phases
+  // (64 B of every stage-1 row instead of 32) and the per-workgroup tables are shared
+  // by twice the threads (PFB_SYNTH_NTP=128 restores the 128-thread shape)
+  static const int ntp_env = std::getenv("PFB_SYNTH_NTP") ? std::atoi(std::getenv("PFB_SYNTH_NTP")) : 0;
+  if constexpr (NF >= 512) {
+    constexpr int P2 = 256 / (NF / synth_first_radix<NF, W>());
+    if (ntp_env != 128 && a.N % (2 * P2) == 0) return launch_sb<NF, W, P2, SPANS, 256>(a, s);
+  }
   constexpr int POPT = NTP / (NF / synth_first_radix<NF, W>());
   static_assert(POPT >= 1, "first pass wider than the workgroup");
   if (a.N % (2 * POPT) == 0) return launch_sb<NF, W, POPT, SPANS>(a, s);
