@@ -480,6 +480,191 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
   }
 }
 
+// ------------------------------------------------------------- LDS-shared register FIR
+// Same sums as fir_window_kernel, organised so that the NU residues reading the same
+// input columns share one workgroup: thread (cl, s) owns column c = c0 + cl of the input
+// viewed as rows of N samples and residue s, i.e. arm n_s(c) (padded (s M - 1 - c) mod N,
+// Bunton (c - s M) mod N; both write channel position N - 1 - c / c).  Each input sample
+// of the workgroup's CW columns is loaded from HBM ONCE into an LDS ring of x rows and
+// read from there by its NU residue threads (fir_window_kernel loads it NU times); every
+// thread keeps its PW-sample window in registers and takes DE new samples per row step q
+// (rows k = NU q + s) from the ring.  U steps per barrier, the next U steps' rows loaded
+// into registers one iteration ahead.
+template <int NU, int DE>
+struct FirLdsShape {
+  static constexpr int CW = NT / NU;                       // columns per workgroup
+  static constexpr int U = DE >= 7 ? 3 : 4;                // row steps per barrier
+  static constexpr int BATCH = U * DE * CW;                // samples staged per iteration
+  static constexpr int NPF = (BATCH + NT - 1) / NT;        // prefetch registers per thread
+  static constexpr int SPAN = 2 * U * DE + DE + 4;         // live ring rows (bound)
+  static constexpr int RR = SPAN <= 32 ? 32 : SPAN <= 64 ? 64 : 128;  // ring rows (pow2)
+  static constexpr int CWP = CW + 1;                       // padded ring row (banks)
+};
+
+template <int PW, int DE, int NU, int VARIANT>
+__global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges) {
+  using SH = FirLdsShape<NU, DE>;
+  constexpr int CW = SH::CW, U = SH::U, RR = SH::RR, CWP = SH::CWP, NPF = SH::NPF;
+  __shared__ v2f ring[RR * CWP];
+  __shared__ int e_ext[2];
+  const int N = a.N, M = a.M;
+  const int chunks = N / CW;
+  const int chunk = blockIdx.x % chunks, rg = blockIdx.x / chunks;  // b and b + chunks: same XCD
+  const int pol = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int cl = tid % CW, s = tid / CW;
+  const int c0 = chunk * CW, c = c0 + cl;
+  const int64_t sM = (int64_t)s * M;
+  int n, ar;
+  if constexpr (VARIANT == kBunton) {
+    n = (int)(((c - sM) % N + N) % N);
+    ar = (int)((sM + n - c) / N);
+  } else {
+    n = (int)(((sM - 1 - c) % N + N) % N);
+    ar = (int)((sM - 1 - c - n) / N);
+  }
+  const int e = VARIANT == kBunton ? ar + PW - 1 : ar;  // newest window row, relative to DE q
+  if (tid == 0) {
+    e_ext[0] = INT32_MAX;
+    e_ext[1] = INT32_MIN;
+  }
+  __syncthreads();
+  atomicMin(&e_ext[0], e);
+  atomicMax(&e_ext[1], e);
+  __syncthreads();
+  const int e_min = e_ext[0], e_max = e_ext[1];
+
+  // this workgroup's row steps q (rows k = NU q + s in [row0, K))
+  const int64_t q_lo = a.row0 / NU, q_hi = (a.K + NU - 1) / NU, nq = q_hi - q_lo;
+  const int64_t q0 = q_lo + nq * rg / ranges, q1 = q_lo + nq * (rg + 1) / ranges;
+  if (q0 >= q1) return;
+
+  // input descriptor from the lowest row the range touches (samples outside [0, n_dat)
+  // read as 0 through the range check; the launcher keeps the extent within a descriptor)
+  const float2* xpol = a.in + pol * a.in_pol_stride;
+  const int64_t rho_min = (int64_t)DE * q0 + e_min - PW;
+  const int64_t b0 = max((int64_t)0, rho_min * N);
+  const int64_t avail = a.n_dat - b0;
+  const __amdgpu_buffer_rsrc_t xr =
+      make_rsrc(xpol + b0, (uint32_t)min(max(avail, (int64_t)0) * 8, kRsrcMaxBytes));
+  auto ld = [&](int64_t rho, int col) {  // x[rho N + col]
+    const int64_t g = rho * N + col;
+    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (uint32_t)((g - b0) * 8), 0, 0);
+    return __builtin_bit_cast(v2f, v);
+  };
+  float f[PW];
+#pragma unroll
+  for (int p = 0; p < PW; ++p) f[p] = a.taps[p * N + n];  // zero-padded to 32 N
+  // window row of tap p at step q: padded DE q + ar - p, Bunton DE q + ar + p
+  auto wrow = [&](int64_t q, int p) -> int64_t {
+    return VARIANT == kBunton ? (int64_t)DE * q + ar + p : (int64_t)DE * q + ar - p;
+  };
+  v2f w[PW];
+#pragma unroll
+  for (int p = 0; p < PW; ++p) w[p] = ld(wrow(q0, p), c);
+  // ring: rows (DE q0 + e_min, DE q0 + e_max] now; each iteration adds U DE rows
+  for (int i = tid; i < (e_max - e_min) * CW; i += NT) {
+    const int64_t rho = (int64_t)DE * q0 + e_min + 1 + i / CW;
+    ring[(int)(rho & (RR - 1)) * CWP + i % CW] = ld(rho, c0 + i % CW);
+  }
+  v2f pf[NPF];
+  auto prefetch = [&](int64_t qi) {  // rows (DE qi + e_max, DE qi + e_max + U DE]
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      const int i = min(tid + j * NT, SH::BATCH - 1);
+      pf[j] = ld((int64_t)DE * qi + e_max + 1 + i / CW, c0 + i % CW);
+    }
+  };
+  prefetch(q0);
+
+  // outputs: Z rows (round trip) or scratch rows at channel position pos
+  const int pos = VARIANT == kBunton ? c : N - 1 - c;
+  float2* sc = a.scratch + (int64_t)pol * (a.K - a.row0) * N + pos;
+  const int zcol = VARIANT == kBunton ? pos : (N - pos) % N;
+  float2* zc = a.z ? a.z + pol * a.z_pol_stride + zcol : nullptr;
+  const float zscale = (float)N * (float)N;
+  auto emit = [&](int64_t k, v2f acc) {
+    if (k < a.row0 || k >= a.K) return;
+    if (!zc) {
+      sc[(k - a.row0) * N] = make_float2(acc.x, acc.y);
+    } else {
+      int64_t t = k;
+      if constexpr (VARIANT != kBunton) {
+        t = k - a.sds;
+        while (t < 0) t += a.K_total;
+      }
+      if (t >= a.z_row0) zc[(t - a.z_row0) * N] = make_float2(zscale * acc.x, zscale * acc.y);
+    }
+  };
+
+#pragma unroll 1
+  for (int64_t qi = q0; qi < q1; qi += U) {
+    // rows of this iteration -> ring, next iteration's rows -> registers
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      const int i = tid + j * NT;
+      if (i < SH::BATCH) {
+        const int64_t rho = (int64_t)DE * qi + e_max + 1 + i / CW;
+        ring[(int)(rho & (RR - 1)) * CWP + i % CW] = pf[j];
+      }
+    }
+    prefetch(qi + U);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = qi + u;
+      if (q < q1) {
+        // same pairing of taps as fir_window_kernel (bit-identical sums)
+        v2f acc0{0.f, 0.f}, acc1{0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < PW; p += 2) {
+          acc0 = __builtin_elementwise_fma(v2f{f[p], f[p]}, w[p], acc0);
+          if (p + 1 < PW) acc1 = __builtin_elementwise_fma(v2f{f[p + 1], f[p + 1]}, w[p + 1], acc1);
+        }
+        emit((int64_t)NU * q + s, acc0 + acc1);
+      }
+      // slide to step q + 1: DE new samples from the ring
+      if constexpr (VARIANT == kBunton) {
+#pragma unroll
+        for (int p = 0; p < PW - DE; ++p) w[p] = w[p + DE];
+#pragma unroll
+        for (int p = PW - DE; p < PW; ++p)
+          w[p] = ring[(int)(wrow(q + 1, p) & (RR - 1)) * CWP + cl];
+      } else {
+#pragma unroll
+        for (int p = PW - 1; p >= DE; --p) w[p] = w[p - DE];
+#pragma unroll
+        for (int p = 0; p < DE; ++p) w[p] = ring[(int)(wrow(q + 1, p) & (RR - 1)) * CWP + cl];
+      }
+    }
+  }
+}
+
+template <int PW, int DE>
+static hipError_t launch_fir_lds_t(const AnalysisArgs& a, hipStream_t s) {
+  constexpr int NU = DE == 7 ? 8 : 4;
+  using SH = FirLdsShape<NU, DE>;
+  const int chunks = a.N / SH::CW;
+  const int64_t nq = (a.K + NU - 1) / NU - a.row0 / NU;
+  static const int target = [] {
+    const char* v = std::getenv("PFB_FIR_LDS_WGS");
+    return v ? std::max(1, std::atoi(v)) : 2048;
+  }();
+  int64_t ranges = std::max<int64_t>(1, std::min<int64_t>(target / chunks, nq / (4 * SH::U)));
+  // one range reads rows [DE q0 + e_min - PW, DE q1 + e_max + 2 U DE]: within a descriptor
+  const int64_t halo_rows = PW + 2 * SH::U * DE + 2 * NU + 4;
+  const int64_t fit_rows = kRsrcMaxBytes / 8 / a.N - halo_rows;
+  if (fit_rows <= 0) return hipErrorInvalidValue;
+  ranges = std::max(ranges, (nq * DE + fit_rows - 1) / fit_rows);
+  if (ranges * chunks > INT32_MAX) return hipErrorInvalidValue;
+  dim3 grid((unsigned)(chunks * ranges), (unsigned)a.n_pol);
+  if (a.variant == kBunton)
+    hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kBunton>), grid, dim3(NT), 0, s, a, (int)ranges);
+  else
+    hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kPadded>), grid, dim3(NT), 0, s, a, (int)ranges);
+  return hipGetLastError();
+}
+
 template <int PW, int DE>
 static hipError_t launch_fir_window_t(const AnalysisArgs& a, hipStream_t s) {
   const int chunks = a.N / NT;
@@ -525,6 +710,18 @@ static hipError_t launch_fir_window_t(const AnalysisArgs& a, hipStream_t s) {
 template <int DE>
 static bool launch_fir_window_de(const AnalysisArgs& a, hipStream_t s, hipError_t* e) {
   if (a.P > 32 || a.P < DE) return false;
+  // the LDS-shared form where NU divides the workgroup (8/7, 4/3); PFB_FIR_LDS=0: A/B
+  static const bool no_lds = std::getenv("PFB_FIR_LDS") && std::atoi(std::getenv("PFB_FIR_LDS")) == 0;
+  if constexpr (DE == 7 || DE == 3) {
+    constexpr int NU = DE == 7 ? 8 : 4;
+    if (!no_lds && a.nu == NU && a.N % (NT / NU) == 0) {
+      if (a.P <= 13) *e = launch_fir_lds_t<13, DE>(a, s);
+      else if (a.P <= 16) *e = launch_fir_lds_t<16, DE>(a, s);
+      else if (a.P <= 25) *e = launch_fir_lds_t<25, DE>(a, s);
+      else *e = launch_fir_lds_t<32, DE>(a, s);
+      return true;
+    }
+  }
   if (a.P <= 13) *e = launch_fir_window_t<13, DE>(a, s);
   else if (a.P <= 16) *e = launch_fir_window_t<16, DE>(a, s);
   else if (a.P <= 25) *e = launch_fir_window_t<25, DE>(a, s);
