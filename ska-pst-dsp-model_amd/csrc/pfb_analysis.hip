@@ -480,23 +480,26 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
   }
 }
 
-// ------------------------------------------------------------- LDS-shared register FIR
+// ------------------------------------------------------------- LDS-shared transposed FIR
 // Same sums as fir_window_kernel, organised so that the NU residues reading the same
 // input columns share one workgroup: thread (cl, s) owns column c = c0 + cl of the input
 // viewed as rows of N samples and residue s, i.e. arm n_s(c) (padded (s M - 1 - c) mod N,
 // Bunton (c - s M) mod N; both write channel position N - 1 - c / c).  Each input sample
 // of the workgroup's CW columns is loaded from HBM ONCE into an LDS ring of x rows and
-// read from there by its NU residue threads (fir_window_kernel loads it NU times); every
-// thread keeps its PW-sample window in registers and takes DE new samples per row step q
-// (rows k = NU q + s) from the ring.  U steps per barrier, the next U steps' rows loaded
-// into registers one iteration ahead.
+// read from there by its NU residue threads (fir_window_kernel loads it NU times).
+// Row step q (rows k = NU q + s) brings DE new samples per thread; in transposed form
+// each new sample is multiplied by every tap it will meet while it slides through the
+// window (taps i + j DE, padded; PW - DE + i - j DE, Bunton) into the accumulators of the
+// outputs q .. q + NJ - 1, so no sample window is kept or shifted: NJ accumulators, the
+// oldest completes every step.  A range starts NJ - 1 steps early (warm-up, no output).
+// U steps per barrier, the next U steps' rows loaded into registers one iteration ahead.
 template <int NU, int DE>
 struct FirLdsShape {
   static constexpr int CW = NT / NU;                       // columns per workgroup
   static constexpr int U = DE >= 7 ? 3 : 4;                // row steps per barrier
   static constexpr int BATCH = U * DE * CW;                // samples staged per iteration
   static constexpr int NPF = (BATCH + NT - 1) / NT;        // prefetch registers per thread
-  static constexpr int SPAN = 2 * U * DE + DE + 4;         // live ring rows (bound)
+  static constexpr int SPAN = 2 * U * DE + DE + NU + 2;    // live ring rows (bound)
   static constexpr int RR = SPAN <= 32 ? 32 : SPAN <= 64 ? 64 : 128;  // ring rows (pow2)
   static constexpr int CWP = CW + 1;                       // padded ring row (banks)
 };
@@ -505,6 +508,7 @@ template <int PW, int DE, int NU, int VARIANT>
 __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges) {
   using SH = FirLdsShape<NU, DE>;
   constexpr int CW = SH::CW, U = SH::U, RR = SH::RR, CWP = SH::CWP, NPF = SH::NPF;
+  constexpr int NJ = (PW + DE - 1) / DE;  // outputs a sample contributes to
   __shared__ v2f ring[RR * CWP];
   __shared__ int e_ext[2];
   const int N = a.N, M = a.M;
@@ -523,7 +527,8 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges)
     n = (int)(((sM - 1 - c) % N + N) % N);
     ar = (int)((sM - 1 - c - n) / N);
   }
-  const int e = VARIANT == kBunton ? ar + PW - 1 : ar;  // newest window row, relative to DE q
+  // newest input row of step q relative to DE q (padded: tap 0; Bunton: tap PW - 1)
+  const int e = VARIANT == kBunton ? ar + PW - 1 : ar;
   if (tid == 0) {
     e_ext[0] = INT32_MAX;
     e_ext[1] = INT32_MIN;
@@ -534,15 +539,16 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges)
   __syncthreads();
   const int e_min = e_ext[0], e_max = e_ext[1];
 
-  // this workgroup's row steps q (rows k = NU q + s in [row0, K))
+  // this workgroup's row steps q (rows k = NU q + s in [row0, K)), plus the warm-up
   const int64_t q_lo = a.row0 / NU, q_hi = (a.K + NU - 1) / NU, nq = q_hi - q_lo;
   const int64_t q0 = q_lo + nq * rg / ranges, q1 = q_lo + nq * (rg + 1) / ranges;
   if (q0 >= q1) return;
+  const int64_t qw = q0 - (NJ - 1);
 
   // input descriptor from the lowest row the range touches (samples outside [0, n_dat)
   // read as 0 through the range check; the launcher keeps the extent within a descriptor)
   const float2* xpol = a.in + pol * a.in_pol_stride;
-  const int64_t rho_min = (int64_t)DE * q0 + e_min - PW;
+  const int64_t rho_min = (int64_t)DE * qw + e_min - DE;
   const int64_t b0 = max((int64_t)0, rho_min * N);
   const int64_t avail = a.n_dat - b0;
   const __amdgpu_buffer_rsrc_t xr =
@@ -552,30 +558,24 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges)
     const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (uint32_t)((g - b0) * 8), 0, 0);
     return __builtin_bit_cast(v2f, v);
   };
+  // taps by (new-sample slot i, lag j): padded i + j DE, Bunton PW - DE + i - j DE
   float f[PW];
 #pragma unroll
   for (int p = 0; p < PW; ++p) f[p] = a.taps[p * N + n];  // zero-padded to 32 N
-  // window row of tap p at step q: padded DE q + ar - p, Bunton DE q + ar + p
-  auto wrow = [&](int64_t q, int p) -> int64_t {
-    return VARIANT == kBunton ? (int64_t)DE * q + ar + p : (int64_t)DE * q + ar - p;
-  };
-  v2f w[PW];
-#pragma unroll
-  for (int p = 0; p < PW; ++p) w[p] = ld(wrow(q0, p), c);
-  // ring: rows (DE q0 + e_min, DE q0 + e_max] now; each iteration adds U DE rows
+  // ring: rows (DE qw + e_min - DE, DE qw + e_max - DE] now; each iteration adds U DE rows
   for (int i = tid; i < (e_max - e_min) * CW; i += NT) {
-    const int64_t rho = (int64_t)DE * q0 + e_min + 1 + i / CW;
+    const int64_t rho = (int64_t)DE * (qw - 1) + e_min + 1 + i / CW;
     ring[(int)(rho & (RR - 1)) * CWP + i % CW] = ld(rho, c0 + i % CW);
   }
   v2f pf[NPF];
-  auto prefetch = [&](int64_t qi) {  // rows (DE qi + e_max, DE qi + e_max + U DE]
+  auto prefetch = [&](int64_t qi) {  // rows (DE (qi - 1) + e_max, DE (qi - 1) + e_max + U DE]
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {
       const int i = min(tid + j * NT, SH::BATCH - 1);
-      pf[j] = ld((int64_t)DE * qi + e_max + 1 + i / CW, c0 + i % CW);
+      pf[j] = ld((int64_t)DE * (qi - 1) + e_max + 1 + i / CW, c0 + i % CW);
     }
   };
-  prefetch(q0);
+  prefetch(qw);
 
   // outputs: Z rows (round trip) or scratch rows at channel position pos
   const int pos = VARIANT == kBunton ? c : N - 1 - c;
@@ -591,20 +591,23 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges)
       int64_t t = k;
       if constexpr (VARIANT != kBunton) {
         t = k - a.sds;
-        while (t < 0) t += a.K_total;
+        if (t < 0) t += a.K_total * ((-t + a.K_total - 1) / a.K_total);
       }
       if (t >= a.z_row0) zc[(t - a.z_row0) * N] = make_float2(zscale * acc.x, zscale * acc.y);
     }
   };
 
+  v2f acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] = v2f{0.f, 0.f};
 #pragma unroll 1
-  for (int64_t qi = q0; qi < q1; qi += U) {
+  for (int64_t qi = qw; qi < q1; qi += U) {
     // rows of this iteration -> ring, next iteration's rows -> registers
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {
       const int i = tid + j * NT;
       if (i < SH::BATCH) {
-        const int64_t rho = (int64_t)DE * qi + e_max + 1 + i / CW;
+        const int64_t rho = (int64_t)DE * (qi - 1) + e_max + 1 + i / CW;
         ring[(int)(rho & (RR - 1)) * CWP + i % CW] = pf[j];
       }
     }
@@ -613,29 +616,24 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t q = qi + u;
-      if (q < q1) {
-        // same pairing of taps as fir_window_kernel (bit-identical sums)
-        v2f acc0{0.f, 0.f}, acc1{0.f, 0.f};
+      // the DE new samples of step q: rows DE q + e - DE + 1 + ii (ii = DE - 1 newest)
+      v2f xn[DE];
+      const int64_t r_new = (int64_t)DE * q + e - DE + 1;
 #pragma unroll
-        for (int p = 0; p < PW; p += 2) {
-          acc0 = __builtin_elementwise_fma(v2f{f[p], f[p]}, w[p], acc0);
-          if (p + 1 < PW) acc1 = __builtin_elementwise_fma(v2f{f[p + 1], f[p + 1]}, w[p + 1], acc1);
+      for (int ii = 0; ii < DE; ++ii) xn[ii] = ring[(int)((r_new + ii) & (RR - 1)) * CWP + cl];
+#pragma unroll
+      for (int ii = 0; ii < DE; ++ii) {
+        // slot i: padded tap p = DE - 1 - ii (row DE q + ar - p), Bunton p = PW - DE + ii
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int p = VARIANT == kBunton ? PW - DE + ii - j * DE : DE - 1 - ii + j * DE;
+          if (p >= 0 && p < PW) acc[j] = __builtin_elementwise_fma(v2f{f[p], f[p]}, xn[ii], acc[j]);
         }
-        emit((int64_t)NU * q + s, acc0 + acc1);
       }
-      // slide to step q + 1: DE new samples from the ring
-      if constexpr (VARIANT == kBunton) {
+      if (q >= q0 && q < q1) emit((int64_t)NU * q + s, acc[0]);
 #pragma unroll
-        for (int p = 0; p < PW - DE; ++p) w[p] = w[p + DE];
-#pragma unroll
-        for (int p = PW - DE; p < PW; ++p)
-          w[p] = ring[(int)(wrow(q + 1, p) & (RR - 1)) * CWP + cl];
-      } else {
-#pragma unroll
-        for (int p = PW - 1; p >= DE; --p) w[p] = w[p - DE];
-#pragma unroll
-        for (int p = 0; p < DE; ++p) w[p] = ring[(int)(wrow(q + 1, p) & (RR - 1)) * CWP + cl];
-      }
+      for (int j = 0; j < NJ - 1; ++j) acc[j] = acc[j + 1];
+      acc[NJ - 1] = v2f{0.f, 0.f};
     }
   }
 }
@@ -651,8 +649,8 @@ static hipError_t launch_fir_lds_t(const AnalysisArgs& a, hipStream_t s) {
     return v ? std::max(1, std::atoi(v)) : 2048;
   }();
   int64_t ranges = std::max<int64_t>(1, std::min<int64_t>(target / chunks, nq / (4 * SH::U)));
-  // one range reads rows [DE q0 + e_min - PW, DE q1 + e_max + 2 U DE]: within a descriptor
-  const int64_t halo_rows = PW + 2 * SH::U * DE + 2 * NU + 4;
+  // one range reads rows [DE (q0 - NJ) + e_min - DE, DE q1 + e_max + 2 U DE]: within a descriptor
+  const int64_t halo_rows = PW + 3 * DE + 2 * SH::U * DE + 2 * NU + 4;
   const int64_t fit_rows = kRsrcMaxBytes / 8 / a.N - halo_rows;
   if (fit_rows <= 0) return hipErrorInvalidValue;
   ranges = std::max(ranges, (nq * DE + fit_rows - 1) / fit_rows);
