@@ -1,7 +1,7 @@
 #!/bin/bash
-# End-of-round GPU session: parity tests, smoke, bench + kernel-trace profile
-# (gpu_round.sh), then the secondary kernels, the C3 kernel trace, the PCIe-inclusive
-# bench and the FETCH/WRITE PMC passes behind bench.py's roofline.traffic.
+# End-of-round GPU session: parity tests (error statistics), smoke, C2 bench + C4 unit bench
+# + kernel trace (gpu_round.sh), then the secondary kernels, the C3 kernel trace, the
+# PCIe-inclusive bench and the FETCH/WRITE PMC passes of the C2 step and of the C3 round trip.
 set -u
 R=$GRAFT_REPO_ROOT
 bash scripts/gpu_round.sh || exit $?
@@ -17,4 +17,7 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 3 --e2e 1 --no-cpu-baselin
 echo "e2e ok"
 rm -rf gpurun_out/pmc_*
 bash scripts/gpu_pmc.sh FETCH_SIZE WRITE_SIZE || exit $?
+mv gpurun_out/pmc_1 gpurun_out/pmc_c2_fetch && mv gpurun_out/pmc_2 gpurun_out/pmc_c2_write
+PMC_PROG="scripts/bench_aux.py --only-mid --reps 2" bash scripts/gpu_pmc.sh FETCH_SIZE WRITE_SIZE || exit $?
+mv gpurun_out/pmc_1 gpurun_out/pmc_c3_fetch && mv gpurun_out/pmc_2 gpurun_out/pmc_c3_write
 echo "pmc ok"

@@ -14,7 +14,8 @@ import sys
 
 
 def short(name):
-    for k in ("analysis_fused", "analysis_stream", "row_fft", "synth_block", "fir_generic", "fir_window"):
+    for k in ("analysis_fused", "analysis_stream", "row_fft", "synth_block", "fir_generic", "fir_window",
+              "fir_lds", "spectral", "tile_transpose"):
         if k in name:
             return name.split("(")[0].replace("void pfb::", "")
     return None
@@ -38,6 +39,7 @@ def bench_name(k):
         # the ZOUT instance (last template argument true) also runs the channel IFFT
         return "analysis+chan_ifft" if k.rstrip(">").endswith("true") else "analysis"
     for key, v in (("analysis_fused", "analysis"), ("fir_generic", "analysis_fir"),
+                   ("fir_lds", "analysis_fir"), ("fir_window", "analysis_fir"),
                    ("row_fft", "synth_chan_ifft"), ("synth_block", "synth_block")):
         if key in k:
             return v
