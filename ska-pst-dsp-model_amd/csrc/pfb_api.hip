@@ -192,6 +192,7 @@ struct pfb_analysis_plan {
   int64_t n_taps = 0;
   bool fused = false;
   DevBuf taps, twN, scratch;
+  DevBuf ftab;  // Bunton: F = [N zeros, taps, N zeros] for the round trip's recomputed rows
   DevBuf zrev;  // padded generic round trip: index reversal (N - i) mod N of the row FFT input
   // streaming (FilterBank.m:13-14 input_buffer / buffered_samples)
   DevBuf carry, work, stage_in, stage_out;
@@ -358,6 +359,11 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
   for (int64_t i = 0; i < d->n_taps; ++i) taps[(size_t)i] = (float)d->taps[i];  // cast(filt, 'single')
   hipError_t e = upload(p->taps, taps);
   if (e == hipSuccess) e = upload(p->twN, twiddles(p->N, -1));
+  if (e == hipSuccess && p->variant == pfb::kBunton) {
+    std::vector<float> f((size_t)(p->P + 2) * p->N, 0.f);
+    for (int64_t i = 0; i < d->n_taps; ++i) f[(size_t)(p->N + i)] = (float)d->taps[i];
+    e = upload(p->ftab, f);
+  }
   if (e == hipSuccess && !p->fused && p->variant == pfb::kPadded) {
     std::vector<int> rev((size_t)p->N);
     for (int i = 0; i < p->N; ++i) rev[(size_t)i] = (p->N - i) % p->N;
@@ -376,6 +382,7 @@ pfb_status pfb_analysis_plan_destroy(pfb_analysis_plan* p) {
   (void)hipSetDevice(p->device);
   p->taps.release();
   p->twN.release();
+  p->ftab.release();
   p->zrev.release();
   p->scratch.release();
   p->carry.release();
@@ -624,9 +631,9 @@ static pfb_status synthesis_chunk(pfb_synthesis_plan* p, const float2* in, int64
 }
 
 // Block kernel over blocks [b0, b0 + nb); Z row 0 is channelised row b0 * keep.
-static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64_t z_ps, int64_t b0,
-                                   int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
-                                   hipStream_t s) {
+static pfb::SynthBlockArgs synth_args(const pfb_synthesis_plan* p, const float2* Z, int64_t z_ps,
+                                      int64_t b0, int64_t nb, float2* out, int64_t out_ps,
+                                      int64_t out_limit) {
   pfb::SynthBlockArgs a{};
   a.Z = Z;
   a.z_pol_stride = z_ps;
@@ -655,6 +662,13 @@ static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64
   a.no_reuse = p->no_reuse;
   a.xcd = p->xcd;
   a.timing_mask = p->timing_mask;
+  return a;
+}
+
+static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64_t z_ps, int64_t b0,
+                                   int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
+                                   hipStream_t s) {
+  const pfb::SynthBlockArgs a = synth_args(p, Z, z_ps, b0, nb, out, out_ps, out_limit);
   {
     ProfScope ps(2, (double)p->n_pol * (nb * p->keep * p->N * 8.0 + nb * p->Lkeep * 8.0), s);
     HIPCHK(pfb::launch_synth_block(a, s));
@@ -1081,6 +1095,56 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
   const float2* x = (const float2*)in;
   float2* y = (float2*)chan;
   if (B == 0) return analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s);
+
+  // Recomputed stage-1 rows (Bunton streaming shapes, launch_synth_fir): the analysis
+  // writes only the channelised product and the block kernel evaluates the FIR sums of
+  // its own columns from the input, so the rows never cross HBM (555 instead of 727 MB
+  // per C2 step).  The output is bit-identical to the fused path below.  Opt-in
+  // (PFB_RT_FIR=1, read per call): measured no faster than the fused path on C2 and 3 %
+  // slower on C4 — the FIR's tile reads cost the synthesis more LDS time than the rows'
+  // HBM traffic saves.
+  const bool rtfir = std::getenv("PFB_RT_FIR") && std::atoi(std::getenv("PFB_RT_FIR")) != 0;
+  if (rtfir && pa->variant == pfb::kBunton && analysis_emits_z(pa) && pa->ftab.p && ps->identity_perm &&
+      !ps->has_cgain && !ps->has_spectral && ps->chunk_blocks <= 0 && off % pa->nu == 0) {
+    pfb::SynthBlockArgs a = synth_args(ps, nullptr, 0, 0, B, (float2*)out, out_ps, olen);
+    a.x = x;
+    a.x_pol_stride = in_ps;
+    a.n_dat = n_dat;
+    a.fir_f = pa->ftab.as<float>();
+    a.fir_nu = pa->nu;
+    a.fir_de = pa->de;
+    a.fir_M = pa->M;
+    a.fir_P = pa->P;
+    a.fir_k0 = off;
+    if (pfb::synth_fir_supported(a)) {
+      // PFB_RT_FIR_CONC=1: the analysis on the plan's own stream, concurrent with the
+      // synthesis (fork/join through events; A/B measurement)
+      const bool conc = std::getenv("PFB_RT_FIR_CONC") && std::atoi(std::getenv("PFB_RT_FIR_CONC")) != 0;
+      hipStream_t sa = s;
+      if (conc) {
+        if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));
+        while (pa->events.size() < 2) {
+          hipEvent_t e;
+          HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+          pa->events.push_back(e);
+        }
+        HIPCHK(hipEventRecord(pa->events[0], s));
+        HIPCHK(hipStreamWaitEvent(pa->aux, pa->events[0], 0));
+        sa = pa->aux;
+      }
+      pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, sa);
+      if (st != PFB_OK) return st;
+      {
+        ProfScope ps_(2, (double)ps->n_pol * B * ((double)ps->keep * pa->M * 8.0 + ps->Lkeep * 8.0), s);
+        HIPCHK(pfb::launch_synth_fir(a, s));
+      }
+      if (conc) {
+        HIPCHK(hipEventRecord(pa->events[1], sa));
+        HIPCHK(hipStreamWaitEvent(s, pa->events[1], 0));
+      }
+      return PFB_OK;
+    }
+  }
 
   // Fused: the analysis kernel also writes the synthesis stage-1 rows (the channel IFFT
   // of every row it produces, taken as N^2 x its FIR sums before the FFT rather than from

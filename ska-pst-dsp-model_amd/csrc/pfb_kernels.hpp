@@ -83,8 +83,19 @@ struct SynthBlockArgs {
   int ranges;              // 0: one workgroup per block; -1 persistent auto; >0 persistent ranges
   int no_reuse;            // 1: re-read the 2 Ov overlap rows from HBM (PFB_SYNTH_NO_REUSE, A/B only)
   int xcd;                 // 1: XCD-aware workgroup -> (phase group, range) order (PFB_SYNTH_XCD)
-  int timing_mask;         // timing experiments only (PFB_TIMING_MASK): bit0 drop Z loads,
-                           // bit1 drop output stores, bit2 drop tw4 loads (results invalid)
+  int timing_mask;         // timing experiments only (PFB_TIMING_MASK): bit0 drop Z loads
+                           // (input loads in launch_synth_fir), bit1 drop output stores, bit2
+                           // drop tw4 loads; launch_synth_fir: bit3 no FIR arithmetic, bit4 no
+                           // input tile store (results invalid)
+  // Round trip with the stage-1 rows recomputed from the input (launch_synth_fir): Z row
+  // t = N^2 v_{k0 + t}, v_k the Bunton FIR sums of the streaming analysis
+  // (analysis_stream_kernel), evaluated from x instead of read from Z.
+  const float2* x;         // [pol][t] analysis input
+  int64_t x_pol_stride;
+  int64_t n_dat;
+  const float* fir_f;      // F = [N zeros, taps (P rows of N), N zeros], (P + 2) N floats
+  int fir_nu, fir_de, fir_M, fir_P;
+  int64_t fir_k0;          // channelised row of Z row 0 (a multiple of fir_nu)
 };
 
 // Synthesis with a non-identity spectral taper (pfb_spectral.hip): blocks [b0, b0 + nb)
@@ -144,5 +155,8 @@ bool chan_ifft_supported(int N);
 hipError_t launch_chan_ifft(const ChanIfftArgs& a, hipStream_t s);
 bool synth_block_supported(int Nf, int W);
 hipError_t launch_synth_block(const SynthBlockArgs& a, hipStream_t s);
+// synthesis stage 2 with the stage-1 rows recomputed from the analysis input (no Z)
+bool synth_fir_supported(const SynthBlockArgs& a);
+hipError_t launch_synth_fir(const SynthBlockArgs& a, hipStream_t s);
 
 }  // namespace pfb

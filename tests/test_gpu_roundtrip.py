@@ -47,6 +47,10 @@ CASES = [
     # emits the synthesis stage-1 rows)
     (256, "4/3", 12, 256, 48, "polyphase_analysis", 2, 1 << 19, 0, 3),
     (256, "8/7", 11, 256, 48, "polyphase_analysis", 1, (1 << 19) + 777, 0, 2),
+    # sample offsets a multiple of nu (where PFB_RT_FIR=1 recomputes the rows)
+    (256, "8/7", 12, 256, 48, "polyphase_analysis", 2, 1 << 19, 0, 9),
+    (256, "4/3", 12, 256, 48, "polyphase_analysis", 2, 1 << 19, 0, 5),
+    (256, "8/7", 11, 256, 48, "polyphase_analysis", 1, (1 << 19) + 777, 0, 1),
     # N > 256: the register-window FIR emits the stage-1 rows (fused with chunk 0)
     (512, "8/7", 12, 128, 16, "polyphase_analysis", 2, 1 << 19, 0, 1),
     (512, "8/7", 12, 128, 16, "polyphase_analysis_padded", 1, 1 << 19, 0, 4),
@@ -332,3 +336,43 @@ def test_c3_full_size_impulse_and_linearity(gpu):
     lhs = y2.cpu().numpy()
     rhs = (0.5 * y1 + 3.0 * y).cpu().numpy()
     assert_pfb_close(lhs, rhs, tol=2e-6, scale=1.0, what="C3 linearity (raw)")
+
+
+RECOMPUTE_CASES = [
+    # (os, taps/chan, n_pol, n_dat, sample_offset): every size where the synthesis
+    # recomputes its stage-1 rows from the input (Bunton, N 256, Nf 256 / Ov 48)
+    ("8/7", 12, 1, 1 << 20, 1),
+    ("8/7", 12, 2, 1 << 19, 17),
+    ("8/7", 11, 1, 300_000, 1),
+    ("4/3", 12, 2, 1 << 19, 1),
+    ("4/3", 12, 1, 200_001, 9),
+    ("8/7", 12, 1, 90_000, 1),    # a handful of blocks: ranges of 0 or 1 block
+    ("8/7", 12, 3, 1 << 18, 1),
+]
+
+
+@pytest.mark.parametrize("case", RECOMPUTE_CASES)
+def test_roundtrip_recomputed_rows_bit_identical(gpu, case, monkeypatch):
+    """The synthesis that evaluates the Bunton FIR sums of its own columns from the input
+    (launch_synth_fir: no stage-1 rows in HBM) gives exactly the output of the fused path
+    that reads them (the default; the analysis kernel writes N^2 v_k): same FMA order,
+    same power-of-two scaling — and the same channelised product.  (The recomputing
+    path is opt-in, PFB_RT_FIR=1: measured no faster)"""
+    import torch
+    pfb = _pfb()
+    os_, tpc, n_pol, n_dat, so = case
+    taps = pfb.design_PFB_FIR_filter(256, os_, tpc)
+    x = _noise_t(torch, gpu, (n_pol, n_dat), 11)
+    ana = pfb.AnalysisPlan(taps, 256, os_, "polyphase_analysis", n_pol, 0)
+    win = pfb.PFBWindow().lookup["tukey"](256, 48)
+    syn = pfb.SynthesisPlan(256, os_, 256, 48, True, 1, True, taps, win, None, n_pol, 0)
+    monkeypatch.setenv("PFB_RT_FIR", "1")
+    chan_new, out_new = pfb.roundtrip(ana, syn, x, sample_offset=so)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("PFB_RT_FIR", "0")
+    chan_old, out_old = pfb.roundtrip(ana, syn, x, sample_offset=so)
+    torch.cuda.synchronize()
+    assert out_new.shape == out_old.shape and out_new.shape[1] > 0
+    assert torch.equal(chan_new, chan_old)
+    assert torch.equal(out_new, out_old), (
+        f"max |diff| {float((out_new - out_old).abs().max()):.3e}")
