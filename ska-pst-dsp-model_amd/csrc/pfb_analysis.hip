@@ -505,7 +505,7 @@ struct FirLdsShape {
 };
 
 template <int PW, int DE, int NU, int VARIANT>
-__global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges) {
+__global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges, int cs, int xcd) {
   using SH = FirLdsShape<NU, DE>;
   constexpr int CW = SH::CW, U = SH::U, RR = SH::RR, CWP = SH::CWP, NPF = SH::NPF;
   constexpr int NJ = (PW + DE - 1) / DE;  // outputs a sample contributes to
@@ -513,11 +513,17 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges)
   __shared__ int e_ext[2];
   const int N = a.N, M = a.M;
   const int chunks = N / CW;
-  const int chunk = blockIdx.x % chunks, rg = blockIdx.x / chunks;  // b and b + chunks: same XCD
+  // XCD-aware order (xcd != 0): consecutive chunks of a range on one XCD, so the input
+  // lines two neighbouring chunks share (the padded round trip's chunks start one column
+  // early) are fetched into one L2; else b and b + chunks (same chunk) share an XCD
+  const int lt = xcd ? xcd_tile(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int chunk = lt % chunks, rg = lt / chunks;
   const int pol = blockIdx.y;
   const int tid = threadIdx.x;
   const int cl = tid % CW, s = tid / CW;
-  const int c0 = chunk * CW, c = c0 + cl;
+  // cs = N - 1 (padded round trip): the chunk's columns start one early, so the Z columns
+  // it writes, (c + 1) mod N, are the aligned run c0 .. c0 + CW - 1 (full 128-B lines)
+  const int c0 = chunk * CW, c = (c0 + cl + cs) % N;
   const int64_t sM = (int64_t)s * M;
   int n, ar;
   if constexpr (VARIANT == kBunton) {
@@ -565,14 +571,14 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges)
   // ring: rows (DE qw + e_min - DE, DE qw + e_max - DE] now; each iteration adds U DE rows
   for (int i = tid; i < (e_max - e_min) * CW; i += NT) {
     const int64_t rho = (int64_t)DE * (qw - 1) + e_min + 1 + i / CW;
-    ring[(int)(rho & (RR - 1)) * CWP + i % CW] = ld(rho, c0 + i % CW);
+    ring[(int)(rho & (RR - 1)) * CWP + i % CW] = ld(rho, (c0 + i % CW + cs) % N);
   }
   v2f pf[NPF];
   auto prefetch = [&](int64_t qi) {  // rows (DE (qi - 1) + e_max, DE (qi - 1) + e_max + U DE]
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {
       const int i = min(tid + j * NT, SH::BATCH - 1);
-      pf[j] = ld((int64_t)DE * (qi - 1) + e_max + 1 + i / CW, c0 + i % CW);
+      pf[j] = ld((int64_t)DE * (qi - 1) + e_max + 1 + i / CW, (c0 + i % CW + cs) % N);
     }
   };
   prefetch(qw);
@@ -656,10 +662,15 @@ static hipError_t launch_fir_lds_t(const AnalysisArgs& a, hipStream_t s) {
   ranges = std::max(ranges, (nq * DE + fit_rows - 1) / fit_rows);
   if (ranges * chunks > INT32_MAX) return hipErrorInvalidValue;
   dim3 grid((unsigned)(chunks * ranges), (unsigned)a.n_pol);
+  // padded round trip: shift the column chunks so the Z stores are line-aligned
+  // (PFB_FIR_ZALIGN=0: unshifted, A/B)
+  static const bool no_zalign = std::getenv("PFB_FIR_ZALIGN") && std::atoi(std::getenv("PFB_FIR_ZALIGN")) == 0;
+  const int cs = (a.variant == kPadded && a.z && !no_zalign) ? a.N - 1 : 0;
+  static const int xcd = std::getenv("PFB_FIR_LDS_XCD") ? std::atoi(std::getenv("PFB_FIR_LDS_XCD")) : 1;
   if (a.variant == kBunton)
-    hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kBunton>), grid, dim3(NT), 0, s, a, (int)ranges);
+    hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kBunton>), grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);
   else
-    hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kPadded>), grid, dim3(NT), 0, s, a, (int)ranges);
+    hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kPadded>), grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);
   return hipGetLastError();
 }
 
