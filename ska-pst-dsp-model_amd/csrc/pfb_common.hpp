@@ -160,6 +160,66 @@ __global__ __launch_bounds__(NT) void row_fft_kernel(RowFftArgs a) {
   block_fft<N, DIR, ROWS, NT>(ld, st, rows, tw, threadIdx.x);
 }
 
+// All passes of FFTPlan<N> after the first (one row, LDS -> ... -> `last`).
+template <int N, int DIR, class Last, int R0, int... Rest>
+__device__ __forceinline__ void run_rest(const LdsRows& lds, const Last& last, const float2* tw, int tid,
+                                         Radices<R0, Rest...>) {
+  static_assert(sizeof...(Rest) > 0, "transform has a single pass");
+  run_passes_impl<N, DIR, 1, NT, R0, Rest...>(lds, last, lds, tw, tid);
+}
+
+// Persistent row FFT for one-row-per-workgroup sizes (N >= 4096 with radix-16 first
+// pass): each workgroup walks a contiguous range of rows (XCD-aware order), stages the
+// twiddle table in LDS once, keeps the permutation / gain of its thread's 16 first-pass
+// columns in registers, and loads row r + 1 into registers while it transforms row r.
+// (The one-shot kernel re-read the 32 KB table from L2 for every one of the 73 400 C3
+// rows and waited for each row's loads with nothing in flight.)
+template <int N, int DIR, bool PERM, bool GAIN>
+__global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
+  static_assert(RowShape<N>::ROWS == 1, "one row per workgroup");
+  constexpr int R = FirstPassOf<N, 1, NT>::R, NB = N / R;
+  static_assert(NB == NT, "one first-pass butterfly per thread");
+  extern __shared__ __attribute__((aligned(16))) float2 smem[];
+  const int pol = blockIdx.y;
+  const int w = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t q0 = a.n_rows * w / gridDim.x, q1 = a.n_rows * (w + 1) / gridDim.x;
+  if (q0 >= q1) return;
+  const int tid = threadIdx.x;
+  LdsRows rows(smem, RowShape<N>::RS);
+  float2* tw = smem + RowShape<N>::RS;
+  for (int m = tid; m < N; m += NT) tw[tw_slot(m)] = a.tw[m];
+  const float2* in = a.in + pol * a.in_pol_stride;
+  int col[R];
+  float g[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = tid + r * NB;
+    col[r] = PERM ? a.perm[i] : i;
+    g[r] = GAIN ? a.cgain[col[r]] : 1.f;
+  }
+  float2 pf[R];
+  auto load_row = [&](int64_t row) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) pf[r] = in[row * N + col[r]];
+  };
+  load_row(q0);
+#pragma unroll 1
+  for (int64_t row = q0; row < q1; ++row) {
+    float2 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = GAIN ? cscale(pf[r], g[r]) : pf[r];
+    load_row(min(row + 1, q1 - 1));  // unconditional: the last row re-reads itself
+    __syncthreads();  // tables / the previous row's last pass done with the LDS row
+    // first pass (radix R, stride 1): no twiddles, outputs j R + r
+    sdft<R, DIR>(v);
+#pragma unroll
+    for (int r = 0; r < R; ++r) rows.store(0, tid * R + r, v[r]);
+    __syncthreads();
+    RowStore st{a.out + pol * a.out_pol_stride, row, a.n_rows, N, a.sds, a.remap, a.scale,
+                a.row_base, a.n_total};
+    run_rest<N, DIR>(rows, st, tw, tid, typename FFTPlan<N>::type{});
+  }
+}
 
 // ======================================================================= launchers
 // Launch through hipExtLaunchKernelGGL when the profiler has armed events (they are

@@ -3,11 +3,29 @@
 // of every channelised row, polyphase_synthesis.m:282-285 factored).
 #include "pfb_common.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace pfb {
 
 template <int N, int DIR, bool PERM, bool GAIN>
 static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s) {
   constexpr int ROWS = RowShape<N>::ROWS;
+  if constexpr (N == 4096) {
+    // persistent workgroups (row_fft_persist_kernel) once there are several rows per
+    // resident workgroup; PFB_ROWFFT_PERSIST=0: one workgroup per row (A/B)
+    static const bool off = std::getenv("PFB_ROWFFT_PERSIST") && std::atoi(std::getenv("PFB_ROWFFT_PERSIST")) == 0;
+    const size_t bytes = ((size_t)RowShape<N>::RS + tw_slots(N)) * sizeof(float2);
+    const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / bytes);
+    const int64_t wgs = (int64_t)cu_count() * per_cu;
+    if (!off && r.n_rows >= 4 * wgs) {
+      auto kern = row_fft_persist_kernel<N, DIR, PERM, GAIN>;
+      hipError_t e = set_lds(kern, bytes);
+      if (e != hipSuccess) return e;
+      dim3 grid((unsigned)std::max<int64_t>(1, wgs / n_pol), (unsigned)n_pol);
+      return launch_kernel(kern, grid, dim3(NT), bytes, s, r);
+    }
+  }
   const size_t bytes = ((size_t)ROWS * RowShape<N>::RS + tw_slots(N)) * sizeof(float2);
   auto kern = row_fft_kernel<N, DIR, PERM, GAIN>;
   hipError_t e = set_lds(kern, bytes);
