@@ -501,15 +501,23 @@ struct FirLdsShape {
   static constexpr int NPF = (BATCH + NT - 1) / NT;        // prefetch registers per thread
   static constexpr int SPAN = 2 * U * DE + DE + NU + 2;    // live ring rows (bound)
   static constexpr int RR = SPAN <= 32 ? 32 : SPAN <= 64 ? 64 : 128;  // ring rows (pow2)
+  static constexpr int MIR = U * DE;                       // mirrored rows past the ring end
   static constexpr int CWP = CW + 1;                       // padded ring row (banks)
 };
 
 template <int PW, int DE, int NU, int VARIANT>
 __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges, int cs, int xcd) {
   using SH = FirLdsShape<NU, DE>;
-  constexpr int CW = SH::CW, U = SH::U, RR = SH::RR, CWP = SH::CWP, NPF = SH::NPF;
+  constexpr int CW = SH::CW, U = SH::U, RR = SH::RR, CWP = SH::CWP, NPF = SH::NPF, MIR = SH::MIR;
   constexpr int NJ = (PW + DE - 1) / DE;  // outputs a sample contributes to
-  __shared__ v2f ring[RR * CWP];
+  // ring rows 0 .. MIR - 1 are mirrored at RR .. RR + MIR - 1, so one iteration's U DE
+  // consecutive rows are read from a single base with immediate offsets (no wrap masks)
+  __shared__ v2f ring[(RR + MIR) * CWP];
+  auto ring_put = [&](int64_t rho, int col, v2f v) {
+    const int m = (int)(rho & (RR - 1));
+    ring[m * CWP + col] = v;
+    if (m < MIR) ring[(m + RR) * CWP + col] = v;
+  };
   __shared__ int e_ext[2];
   const int N = a.N, M = a.M;
   const int chunks = N / CW;
@@ -571,7 +579,7 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges,
   // ring: rows (DE qw + e_min - DE, DE qw + e_max - DE] now; each iteration adds U DE rows
   for (int i = tid; i < (e_max - e_min) * CW; i += NT) {
     const int64_t rho = (int64_t)DE * (qw - 1) + e_min + 1 + i / CW;
-    ring[(int)(rho & (RR - 1)) * CWP + i % CW] = ld(rho, (c0 + i % CW + cs) % N);
+    ring_put(rho, i % CW, ld(rho, (c0 + i % CW + cs) % N));
   }
   v2f pf[NPF];
   auto prefetch = [&](int64_t qi) {  // rows (DE (qi - 1) + e_max, DE (qi - 1) + e_max + U DE]
@@ -597,7 +605,7 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges,
       int64_t t = k;
       if constexpr (VARIANT != kBunton) {
         t = k - a.sds;
-        if (t < 0) t += a.K_total * ((-t + a.K_total - 1) / a.K_total);
+        while (t < 0) t += a.K_total;  // once, unless the series is shorter than sds rows
       }
       if (t >= a.z_row0) zc[(t - a.z_row0) * N] = make_float2(zscale * acc.x, zscale * acc.y);
     }
@@ -614,19 +622,20 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges,
       const int i = tid + j * NT;
       if (i < SH::BATCH) {
         const int64_t rho = (int64_t)DE * (qi - 1) + e_max + 1 + i / CW;
-        ring[(int)(rho & (RR - 1)) * CWP + i % CW] = pf[j];
+        ring_put(rho, i % CW, pf[j]);
       }
     }
     prefetch(qi + U);
     __syncthreads();
+    // this iteration's rows DE qi + e - DE + 1 + [0, U DE): one base, immediate offsets
+    const v2f* rb = ring + (int)(((int64_t)DE * qi + e - DE + 1) & (RR - 1)) * CWP + cl;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t q = qi + u;
       // the DE new samples of step q: rows DE q + e - DE + 1 + ii (ii = DE - 1 newest)
       v2f xn[DE];
-      const int64_t r_new = (int64_t)DE * q + e - DE + 1;
 #pragma unroll
-      for (int ii = 0; ii < DE; ++ii) xn[ii] = ring[(int)((r_new + ii) & (RR - 1)) * CWP + cl];
+      for (int ii = 0; ii < DE; ++ii) xn[ii] = rb[(u * DE + ii) * CWP];
 #pragma unroll
       for (int ii = 0; ii < DE; ++ii) {
         // slot i: padded tap p = DE - 1 - ii (row DE q + ar - p), Bunton p = PW - DE + ii
