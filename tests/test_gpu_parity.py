@@ -156,6 +156,22 @@ def test_analysis_padded_mid(gpu):
     assert_pfb_close(got.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("variant", ["polyphase_analysis", "polyphase_analysis_padded"])
+def test_analysis_4096_persistent_row_fft(gpu, variant):
+    """4096 channels with more than 2048 output rows: the row FFT after the FIR runs as
+    row_fft_persist_kernel (contiguous row ranges per workgroup, next row prefetched),
+    compared with the oracle (the C3 test at 2^22 samples stays below that row count)."""
+    import torch
+    pfb = _pfb()
+    taps = np.random.default_rng(41).standard_normal(4096 * 12 + 1) / 64.0
+    n_dat = 2100 * 3584 + 13 * 4096
+    x = _noise(np.random.default_rng(42), (1, 1, n_dat))
+    ref = getattr(orc, variant)(x, taps, 4096, "8/7")
+    assert ref.shape[2] >= 2100
+    got = getattr(pfb, variant)(torch.from_numpy(x).to(gpu), taps, 4096, "8/7")
+    assert_pfb_close(got.cpu().numpy(), ref, what=f"{variant} 4096 ch, {ref.shape[2]} rows")
+
+
 def test_analysis_short_input(gpu):
     """n_dat shorter than the filter: zero output rows (polyphase_analysis.m:62)."""
     pfb = _pfb()
@@ -231,6 +247,18 @@ def test_synthesis_baseline_shapes(gpu, N, os_, nf, ov, blocks):
     x = _noise(np.random.default_rng(N + blocks), (1, N, blocks * keep + 2 * ov + 3))
     got, ref = _synth_case(pfb, x, 1, nf, os_, 1, taps, ov, "tukey")
     assert_pfb_close(got, ref, what=f"synthesis N={N} {os_}")
+
+
+@pytest.mark.parametrize("taper,combine", [("tukey", 1), ("hann", 1), ("tukey", 2)])
+def test_synthesis_4096_persistent_chan_ifft(gpu, taper, combine):
+    """4096-channel synthesis with more than 2048 channelised rows in one chunk: the
+    stage-1 channel IFFT runs as row_fft_persist_kernel, plain, with the temporal 'hann'
+    per-channel gain (GAIN) and with the combine permutation (PERM)."""
+    pfb = _pfb()
+    taps = _taps("mid")
+    x = _noise(np.random.default_rng(43), (1, 4096, 8 * 256 + 256 + 3))
+    got, ref = _synth_case(pfb, x, 1, 512, "8/7", 1, taps, 128, taper, combine=combine)
+    assert_pfb_close(got, ref, what=f"synthesis 4096 ch, {taper}, combine {combine}")
 
 
 def test_synthesis_chunking_invariant(gpu):
