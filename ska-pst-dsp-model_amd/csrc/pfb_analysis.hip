@@ -182,7 +182,13 @@ struct StreamShape {
 // ZOUT (round trip): each step's channelised rows are also inverse-transformed across
 // channels in LDS and written as synthesis stage-1 rows (AnalysisArgs::z), so the
 // synthesis does not re-read them from HBM.
-template <int N, int P, int NU, int DE, bool ZOUT>
+// LCBF: the SKA-Low CBF PST filterbank (polyphase_analysis_lowcbf.m / PSTFilterbank.m,
+// N 256, M 192, 12 taps) through the same FIR: its FFT of the UNshifted sums times the
+// derotation i^{k (j - 128)} equals the FFT of the Bunton-shifted sums v_k (the shift
+// r = 192 k mod 256 is a multiple of 64, e^{-2 pi i f r / 256} = i^{k f}, exact), and
+// fftshift + the 216-channel selection is output channel c = (f - 148) mod 256 < 216,
+// scaled by 2^12 (LowCbfArgs::scale).  Leading pre-padding zeros via AnalysisArgs::pad.
+template <int N, int P, int NU, int DE, bool ZOUT, bool LCBF = false>
 __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
   using SH = StreamShape<N, P, NU, DE>;
   constexpr int M = SH::M, PE = SH::PE, QS = SH::QS, T = SH::T, NEW = SH::NEW, WIN = SH::WIN;
@@ -199,17 +205,23 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
   // input column c from row DE q_first on; range-checked buffer loads return 0 past n_dat
   const int64_t row_first = (int64_t)DE * (q_lo + st0 * QS);
   const float2* xpol = a.in + pol * a.in_pol_stride;
-  const int64_t avail = a.n_dat - row_first * N;
+  // window row r, column c is x[(row_first + r) N + c - pad]: the descriptor starts at the
+  // first real sample the range reads; pre-padding rows give negative offsets, which wrap
+  // past the range check and read as zeros
+  const int64_t g0 = row_first * N - a.pad;
+  const int64_t gb = max(g0, (int64_t)0);
+  const int shift = (int)(g0 - gb);
+  const int64_t avail = a.n_dat - gb;
   // the launcher sizes the ranges so that a workgroup's rows span <= kRsrcMaxBytes
   // (launch_stream); the min() only bounds the series tail beyond the range
   uint32_t nbytes = (uint32_t)min(max(avail, (int64_t)0) * 8, kRsrcMaxBytes);
   if (a.timing_mask & 1) nbytes = 0;
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(xpol + row_first * N, nbytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(xpol + gb, nbytes);
   // rows past the last window of the range (the unconditional last prefetch) re-read the
   // last row instead: an L2 hit rather than HBM traffic nobody uses
   const int r_last = (int)(st1 - st0 - 1) * NEW + WIN - 1;
   auto ld = [&](int r) {  // window row r (relative to row_first)
-    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (min(r, r_last) * N + c) * 8, 0, 0);
+    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (uint32_t)((min(r, r_last) * N + c + shift) * 8), 0, 0);
     return __builtin_bit_cast(v2f, v);
   };
   // (re, im) as a packed pair: one v_pk_fma_f32 per complex x real tap MAC
@@ -278,8 +290,13 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
       });
     });
     __syncthreads();
-    const BufRowStore st = BufRowStore::rows(opol, k0, T, a.row0, a.K, N, (float)N);
-    block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
+    if constexpr (LCBF) {
+      const LcbfRowStore st = LcbfRowStore::rows(opol, k0, T, a.row0, a.K, a.lcbf_scale);
+      block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
+    } else {
+      const BufRowStore st = BufRowStore::rows(opol, k0, T, a.row0, a.K, N, (float)N);
+      block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
+    }
 #pragma unroll
     for (int i = 0; i < PE - 1; ++i) win[i] = win[i + NEW];
 #pragma unroll
@@ -776,10 +793,11 @@ static hipError_t launch_fused(const AnalysisArgs& a, hipStream_t s) {
   return launch_kernel(kern, grid, dim3(NT), bytes, s, a);
 }
 
-template <int N, int P, int NU, int DE>
+template <int N, int P, int NU, int DE, bool LCBF = false>
 static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
   using SH = StreamShape<N, P, NU, DE>;
-  auto kern = a.z ? analysis_stream_kernel<N, P, NU, DE, true> : analysis_stream_kernel<N, P, NU, DE, false>;
+  auto kern = LCBF ? analysis_stream_kernel<N, P, NU, DE, false, true>
+              : a.z ? analysis_stream_kernel<N, P, NU, DE, true> : analysis_stream_kernel<N, P, NU, DE, false>;
   hipError_t e = set_lds(kern, SH::lds_bytes);
   if (e != hipSuccess) return e;
   const int64_t q_lo = a.row0 / NU;
@@ -830,6 +848,11 @@ template <int N>
 static hipError_t launch_fused_v(const AnalysisArgs& a, hipStream_t s) {
   if (a.variant == kBunton) return launch_fused_p<N, kBunton>(a, s);
   return launch_fused_p<N, kPadded>(a, s);
+}
+
+hipError_t launch_lowcbf_stream(const AnalysisArgs& a, hipStream_t s) {
+  if (a.N != 256 || a.M != 192 || a.P != 12 || a.nu != 4) return hipErrorInvalidValue;
+  return launch_stream<256, 12, 4, 3, true>(a, s);
 }
 
 bool analysis_supported(int N, int P, int variant, bool* fused) {

@@ -62,6 +62,28 @@ struct BufRowStore {
 };
 
 
+// LowCBF output rows (216 of the 256 FFT bins, fftshifted): bin f of row `row` is channel
+// c = (f - 148) mod 256 of output row k0 + row when c < 216 (polyphase_analysis_lowcbf.m /
+// PSTFilterbank.m:35-44); other bins and rows outside [k_lo, k_hi) are dropped by the
+// buffer range check.
+struct LcbfRowStore {
+  static constexpr bool kIsLds = false;
+  __amdgpu_buffer_rsrc_t r;
+  int lo;
+  float scale;
+  __device__ __forceinline__ void store(int row, int f, float2 v) const {
+    const int c = (f + 108) & 255;
+    const uint32_t off = (row >= lo && c < 216) ? (uint32_t)((row * 216 + c) * 8) : 0xFFFFFFF0u;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v, scale)), r, off, 0, 0);
+  }
+  __device__ __forceinline__ static LcbfRowStore rows(float2* base, int64_t k0, int T, int64_t k_lo,
+                                                       int64_t k_hi, float scale) {
+    const int64_t hi = min(max(k_hi - k0, (int64_t)0), (int64_t)T);
+    const int lo = (int)min(max(k_lo - k0, (int64_t)0), (int64_t)T);
+    return LcbfRowStore{make_rsrc(base + k0 * 216, (uint32_t)(hi * 216 * 8)), lo, scale};
+  }
+};
+
 // Row loader of the first FFT pass.  Rows past the end are clamped to the last valid
 // row (their results are never stored), so every load is unconditional and the
 // compiler can issue them back to back.

@@ -42,7 +42,13 @@ struct AnalysisArgs {
   // z_row0 = 0) and the row FFT makes the channelised rows from them through this
   // index reversal (padded variant; null for Bunton) — see fir_window_kernel
   const int* zrev;
+  // leading zeros in front of `in` (the LowCBF wrapper's one-time pre-padding) — the
+  // streaming kernel reads x[r N + c - pad] (zero for negative indices); 0 otherwise
+  int64_t pad;
+  float lcbf_scale;  // LowCBF streaming path: output scale (2^12)
 };
+// SKA-Low CBF PST filterbank through the streaming analysis kernel (pfb_analysis.hip)
+hipError_t launch_lowcbf_stream(const AnalysisArgs& a, hipStream_t s);
 // analysis kernels that can also emit the synthesis stage-1 rows (see AnalysisArgs::z)
 bool analysis_can_emit_z(const AnalysisArgs& a);
 

@@ -18,6 +18,8 @@
 #include "pfb_common.hpp"
 #include "pfb_pair.hpp"
 
+#include <cstdlib>
+
 namespace pfb {
 
 namespace {
@@ -123,6 +125,31 @@ __global__ __launch_bounds__(NT) void lowcbf_kernel(LowCbfArgs a) {
 
 hipError_t launch_lowcbf(const LowCbfArgs& a, hipStream_t s) {
   if (a.K <= 0) return hipSuccess;
+  // streaming path (analysis_stream_kernel<256, 12, 4, 3, LCBF>): persistent workgroups,
+  // each input sample loaded once; PFB_LOWCBF_STREAM=0 keeps the one-shot kernel below
+  static const bool one_shot = std::getenv("PFB_LOWCBF_STREAM") && std::atoi(std::getenv("PFB_LOWCBF_STREAM")) == 0;
+  if (!one_shot) {
+    AnalysisArgs b{};
+    b.in = a.in;
+    b.in_pol_stride = a.in_pol_stride;
+    b.n_dat = a.n_dat;
+    b.out = a.out;
+    b.out_pol_stride = a.out_pol_stride;
+    b.row0 = 0;
+    b.K = a.K;
+    b.K_total = a.K;
+    b.n_pol = a.n_pol;
+    b.N = LN;
+    b.M = LM;
+    b.P = LP;
+    b.nu = 4;
+    b.variant = kBunton;
+    b.taps = a.taps;
+    b.twN = a.tw;
+    b.pad = a.pad;
+    b.lcbf_scale = a.scale;
+    return launch_lowcbf_stream(b, s);
+  }
   static_assert(NT == LN, "one thread per polyphase arm");
   const size_t bytes = ((size_t)LROWS * lds_row(LN) + tw_slots(LN)) * sizeof(float2);
   hipError_t e = set_lds(lowcbf_kernel, bytes);
