@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--skip-mid", action="store_true")
     ap.add_argument("--only-mid", action="store_true")
+    ap.add_argument("--only-twostage", action="store_true")
     ap.add_argument("--cpu", action="store_true",
                     help="also time the NumPy oracle (1 core) on bounded samples of each config")
     args = ap.parse_args()
@@ -63,6 +64,8 @@ def main():
         cpu_baselines(pfb)
     if args.only_mid:
         return mid(torch, pfb, noise, dev)
+    if args.only_twostage:
+        return twostage(torch, pfb, noise, args.reps)
     # ---- C2' (4/3) round trip
     taps43 = pfb.design_PFB_FIR_filter(256, "4/3", 12)
     n = 1 << 24
@@ -106,6 +109,16 @@ def main():
     emit("quantize (moments + round)", ms, 3 * y.numel() * 8)
 
     # ---- two-stage analysis: 256 ch, then 256 ch over each (batched)
+    twostage(torch, pfb, noise, 3)
+
+    # ---- C3 SKA-Mid padded round trip
+    if not args.skip_mid:
+        del x, x2, raw8, raw32, y, rows, chan, out
+        torch.cuda.empty_cache()
+        mid(torch, pfb, noise, dev)
+
+
+def twostage(torch, pfb, noise, reps):
     taps87 = pfb.design_PFB_FIR_filter(256, "8/7", 12)
     cfg = dict(analysis_function="polyphase_analysis", filt_coeff=taps87, channels=256,
                os_factor="8/7")
@@ -113,16 +126,10 @@ def main():
     xs = noise(1, 1, 1 << 24)
     ts.execute(xs)
     ts2 = pfb.TwoStageFilterBank(cfg)
-    ms = timeit(torch, lambda: ts2.execute(xs), 3)
+    ms = timeit(torch, lambda: ts2.execute(xs), reps)
     emit("TwoStageFilterBank 256x256 (stream call)", ms, 16 * (1 + 8 / 7) * (1 << 24),
          msamples_per_s=round((1 << 24) / ms / 1e3, 1),
          note="bytes: the two analyses' input+output, excluding the corner turn")
-
-    # ---- C3 SKA-Mid padded round trip
-    if not args.skip_mid:
-        del x, x2, raw8, raw32, y, rows, chan, out
-        torch.cuda.empty_cache()
-        mid(torch, pfb, noise, dev)
 
 
 def cpu_baselines(pfb):

@@ -868,8 +868,13 @@ bool analysis_can_emit_z(const AnalysisArgs& a) {
   return analysis_supported(a.N, a.P, a.variant, &fused) && !fused && fir_window_applies(a);
 }
 
+bool analysis_takes_offset(const AnalysisArgs& a) {
+  return stream_shape(a) && std::getenv("PFB_ANALYSIS_NO_STREAM") == nullptr;
+}
+
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
   if (a.K <= a.row0) return hipSuccess;
+  if (a.pad != 0 && !analysis_takes_offset(a)) return hipErrorInvalidValue;
   if (a.z && !analysis_can_emit_z(a)) return hipErrorInvalidValue;
   bool fused = false;
   if (!analysis_supported(a.N, a.P, a.variant, &fused)) return hipErrorInvalidValue;

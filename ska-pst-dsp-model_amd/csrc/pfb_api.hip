@@ -210,7 +210,7 @@ struct pfb_analysis_plan {
 static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
                                float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
                                int64_t K_total, hipStream_t s, float2* z = nullptr,
-                               int64_t z_ps = 0, int64_t z_row0 = 0) {
+                               int64_t z_ps = 0, int64_t z_row0 = 0, int64_t pad = 0) {
   if (K_end <= row0) return PFB_OK;
   if (p->variant == pfb::kLowCbf) {
     pfb::LowCbfArgs l{};
@@ -251,6 +251,7 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   a.taps = p->taps.as<float>();
   a.twN = p->twN.as<float2>();
   a.zrev = p->zrev.p ? p->zrev.as<int>() : nullptr;
+  a.pad = pad;  // `in` starts `pad` samples into the series (streaming kernel only)
   a.scratch = nullptr;
   if (!p->fused && !z) {
     HIPCHK(p->scratch.ensure((size_t)p->n_pol * (K_end - row0) * p->N * sizeof(float2)));
@@ -267,6 +268,17 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   ProfScope ps(z ? 3 : 0, bytes, s, p->fused);  // generic path = FIR + row FFT launches
   HIPCHK(pfb::launch_analysis(a, s));
   return PFB_OK;
+}
+
+// the plan's analysis runs on the streaming kernel, which takes a read offset (pad)
+static bool analysis_offset_ok(const pfb_analysis_plan* p) {
+  pfb::AnalysisArgs a{};
+  a.variant = p->variant;
+  a.N = p->N;
+  a.M = p->M;
+  a.P = p->P;
+  a.nu = p->nu;
+  return pfb::analysis_takes_offset(a);
 }
 
 static bool analysis_emits_z(const pfb_analysis_plan* p) {
@@ -443,6 +455,49 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
   hipStream_t s = (hipStream_t)stream;
   const int64_t total = p->buffered + n_in;
   const hipMemcpyKind kin = mem == PFB_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  {
+    // Carry without the concatenation copy (streaming analysis kernel, device input):
+    // rows k >= ceil(B / M) read only the new input, so they run on it in place with the
+    // carried B samples as a read offset (AnalysisArgs::pad); the few rows before that run
+    // on a small stitched buffer of the carry and the head of the input.  The result is the
+    // same per row as the concatenated run (same kernel, same samples).
+    const int64_t B = p->buffered;
+    const int64_t K = analysis_K(p, total);
+    const int64_t Kt = K - (K % p->nu);
+    const int64_t input_idat = (Kt * p->N * p->de) / p->nu;
+    static const bool no_split = std::getenv("PFB_FB_NO_SPLIT") != nullptr;  // A/B
+    if (!no_split && mem == PFB_MEM_DEVICE && B > 0 && p->variant == pfb::kBunton && analysis_offset_ok(p) &&
+        input_idat >= B && p->lowcbf_pad == false) {
+      if (n_out) *n_out = Kt;
+      if (Kt > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld rows",
+                                (long long)cap, (long long)Kt);
+      const int64_t M = p->M, PN = (int64_t)p->P * p->N;
+      const int64_t k_split = std::min(Kt, (B + M - 1) / M);
+      if (k_split > 0) {
+        const int64_t L = std::min(total, (k_split - 1) * M + PN);
+        HIPCHK(p->work.ensure((size_t)p->n_pol * L * sizeof(float2)));
+        float2* wk = p->work.as<float2>();
+        HIPCHK(copy_pols(wk, L, p->carry.as<float2>(), B, std::min(B, L), p->n_pol, hipMemcpyDeviceToDevice, s));
+        if (L > B) HIPCHK(copy_pols(wk + B, L, (const float2*)in, in_ps, L - B, p->n_pol, hipMemcpyDeviceToDevice, s));
+        pfb_status st = analysis_run(p, wk, L, L, (float2*)out, out_ps, 0, k_split, K, s);
+        if (st != PFB_OK) return st;
+      }
+      if (Kt > k_split) {
+        pfb_status st = analysis_run(p, (const float2*)in, in_ps, n_in, (float2*)out, out_ps, k_split, Kt, K, s,
+                                     nullptr, 0, 0, B);
+        if (st != PFB_OK) return st;
+      }
+      // carry = input(:, :, input_idat + 1 : end): all of it lies in the new input
+      const int64_t nb = total - input_idat;
+      if (nb > 0) {
+        HIPCHK(p->carry.ensure((size_t)p->n_pol * nb * sizeof(float2)));
+        HIPCHK(copy_pols(p->carry.as<float2>(), nb, (const float2*)in + (input_idat - B), in_ps, nb, p->n_pol,
+                         hipMemcpyDeviceToDevice, s));
+      }
+      p->buffered = std::max<int64_t>(nb, 0);
+      return PFB_OK;
+    }
+  }
   // input = cat(3, input_buffer, input)   (FilterBank.m:85-88); with nothing buffered and
   // the input already on the device the kernels read it in place (no copy)
   const float2* w;

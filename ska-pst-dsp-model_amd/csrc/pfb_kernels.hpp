@@ -51,6 +51,8 @@ struct AnalysisArgs {
 hipError_t launch_lowcbf_stream(const AnalysisArgs& a, hipStream_t s);
 // analysis kernels that can also emit the synthesis stage-1 rows (see AnalysisArgs::z)
 bool analysis_can_emit_z(const AnalysisArgs& a);
+// analysis shapes whose kernel reads with an input offset (AnalysisArgs::pad)
+bool analysis_takes_offset(const AnalysisArgs& a);
 
 // Synthesis stage 1: per channelised time row, N-point inverse DFT across channels
 // (after the combine permutation and per-channel gain).  See DESIGN.md §synthesis.

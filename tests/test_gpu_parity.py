@@ -346,6 +346,36 @@ def test_filterbank_stream_equals_one_shot(gpu):
     assert torch.equal(streamed, whole[:, :, :streamed.shape[2]])
 
 
+@pytest.mark.parametrize("os_,tpc", [("8/7", 12), ("4/3", 12), ("8/7", 11)])
+def test_filterbank_stream_carry_in_place(gpu, os_, tpc):
+    """Streaming FilterBank on the 256-channel streaming kernel with carried samples: the
+    rows that read only the new input run on it in place (the carry as a read offset),
+    the first ones on a small stitched buffer (pfb_filterbank_execute).  Chunks include
+    ones shorter than the carry (the concatenating path) and two polarisations; the
+    result equals the one-shot analysis bit for bit and the streaming oracle at 1e-6."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, os_, tpc)
+    cfg = dict(analysis_function="polyphase_analysis", filt_coeff=taps, channels=256,
+               os_factor=os_)
+    n_tot = 70000 + 5 + 3001 + 40000 + 123457
+    x = torch.from_numpy(_noise(np.random.default_rng(43), (2, 1, n_tot))).cuda()
+    fb = pfb.FilterBank(cfg)
+    ofb = orc.FilterBankOracle(taps, 256, os_)
+    parts, a = [], 0
+    for n in (70000, 5, 3001, 40000, 123457):
+        fb, y = fb.execute(x[:, :, a:a + n])
+        ref = ofb.execute(x[:, :, a:a + n].cpu().numpy())
+        assert y.shape == ref.shape and fb.buffered_samples == ofb.buffered_samples
+        if ref.size:
+            assert_pfb_close(y.cpu().numpy(), ref, what=f"stream chunk {n}")
+        parts.append(y)
+        a += n
+    streamed = torch.cat(parts, dim=2)
+    whole = pfb.polyphase_analysis(x, taps, 256, os_)
+    assert torch.equal(streamed, whole[:, :, :streamed.shape[2]])
+
+
 def test_inverse_filterbank_streaming_matches_oracle(gpu):
     pfb = _pfb()
     taps = _taps("test")
