@@ -680,7 +680,6 @@ class InverseFilterBankOracle:
         x = np.asarray(x)
         if self.buffered_samples > 0:
             x = np.concatenate([self.input_buffer, x], axis=2)
-            self.buffered_samples = 0
         n_pol, n_chan, n_dat = x.shape
         spans = not self.critical
         dr = bool(self.deripple) if self.honour_deripple else False
@@ -697,6 +696,11 @@ class InverseFilterBankOracle:
         if rem != 0:
             buffered = buffered + modu - rem
             input_idat = n_dat - buffered
+            if input_idat < 0:
+                # InverseFilterBank.m:104-122: no complete block and the carry rounded past
+                # the data -> input(:, :, input_idat+1:end) indexes before the first sample
+                # (the Matlab rounding loop never settles); reject, state unchanged
+                raise ValueError("InverseFilterBank: carry rounded past the data")
             output_ndat = input_idat * Fraction(n_chan * de, nu)
             out = out[:, :, :int(math.floor(output_ndat))]
         self.buffered_samples = int(buffered)

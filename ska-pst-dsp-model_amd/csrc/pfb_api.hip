@@ -166,8 +166,16 @@ hipError_t copy_pols(float2* dst, int64_t dps, const float2* src, int64_t sps, i
                      hipMemcpyKind kind, hipStream_t s) {
   if (n <= 0 || n_pol <= 0) return hipSuccess;
   if (n_pol == 1) return hipMemcpyAsync(dst, src, n * sizeof(float2), kind, s);
-  return hipMemcpy2DAsync(dst, dps * sizeof(float2), src, sps * sizeof(float2), n * sizeof(float2),
-                          n_pol, kind, s);
+  if (kind == hipMemcpyDeviceToDevice) return pfb::launch_copy_rows(dst, dps, src, sps, n, n_pol, s);
+  hipError_t e = hipMemcpy2DAsync(dst, dps * sizeof(float2), src, sps * sizeof(float2), n * sizeof(float2),
+                                  n_pol, kind, s);
+  if (e == hipSuccess) return e;
+  (void)hipGetLastError();  // large row pitches: one copy per row instead
+  for (int q = 0; q < n_pol; ++q) {
+    e = hipMemcpyAsync(dst + q * dps, src + q * sps, n * sizeof(float2), kind, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace
@@ -660,15 +668,20 @@ static pfb_status synthesis_spectral(pfb_synthesis_plan* p, const float2* in, in
 
 // Blocks [b0, b0 + nb) of a call: channel IFFT of their rows into Z, then the block
 // kernel.  `in` is the call's first channelised row (sample_offset applied).
+// (row_shift: `in` holds the call's channelised rows from row row_shift on — a streaming
+// call whose carried rows are not in front of it; blocks b0.. must not read before it)
 static pfb_status synthesis_chunk(pfb_synthesis_plan* p, const float2* in, int64_t in_ps, int64_t b0,
                                   int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
-                                  hipStream_t s) {
-  if (p->has_spectral) return synthesis_spectral(p, in, in_ps, b0, nb, out, out_ps, out_limit, s);
+                                  hipStream_t s, int64_t row_shift = 0) {
+  if (p->has_spectral) {
+    if (row_shift != 0) return fail(PFB_ERR_UNSUPPORTED, "row shift with a spectral taper");
+    return synthesis_spectral(p, in, in_ps, b0, nb, out, out_ps, out_limit, s);
+  }
   const int64_t rows = nb * p->keep + 2 * (int64_t)p->Ov;
   HIPCHK(p->Z.ensure((size_t)p->n_pol * rows * p->N * sizeof(float2)));
   float2* Z = p->Z.as<float2>();
   pfb::ChanIfftArgs c{};
-  c.in = in + b0 * p->keep * p->N;
+  c.in = in + (b0 * p->keep - row_shift) * p->N;
   c.in_pol_stride = in_ps;
   c.out = Z;
   c.out_pol_stride = rows * p->N;
@@ -742,17 +755,23 @@ static int64_t synthesis_chunk_blocks(const pfb_synthesis_plan* p, int64_t B) {
   return std::min<int64_t>(CB, B);
 }
 
-static pfb_status synthesis_run(pfb_synthesis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
-                                float2* out, int64_t out_ps, int64_t out_limit, hipStream_t s) {
-  const int64_t B = synth_blocks(p, n_dat);
-  if (B == 0) return PFB_OK;
-  const int64_t CB = synthesis_chunk_blocks(p, B);
-  for (int64_t b0 = 0; b0 < B; b0 += CB) {
-    pfb_status st = synthesis_chunk(p, in, in_ps, b0, std::min<int64_t>(CB, B - b0), out, out_ps,
-                                    out_limit, s);
+// blocks [b_lo, b_hi) in chunks (see synthesis_chunk for row_shift)
+static pfb_status synthesis_range(pfb_synthesis_plan* p, const float2* in, int64_t in_ps, int64_t b_lo,
+                                  int64_t b_hi, float2* out, int64_t out_ps, int64_t out_limit,
+                                  hipStream_t s, int64_t row_shift = 0) {
+  if (b_hi <= b_lo) return PFB_OK;
+  const int64_t CB = synthesis_chunk_blocks(p, b_hi - b_lo);
+  for (int64_t b0 = b_lo; b0 < b_hi; b0 += CB) {
+    pfb_status st = synthesis_chunk(p, in, in_ps, b0, std::min<int64_t>(CB, b_hi - b0), out, out_ps,
+                                    out_limit, s, row_shift);
     if (st != PFB_OK) return st;
   }
   return PFB_OK;
+}
+
+static pfb_status synthesis_run(pfb_synthesis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
+                                float2* out, int64_t out_ps, int64_t out_limit, hipStream_t s) {
+  return synthesis_range(p, in, in_ps, 0, synth_blocks(p, n_dat), out, out_ps, out_limit, s);
 }
 
 extern "C" {
@@ -1044,6 +1063,61 @@ pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* p, const pfb_cf32*
   const int N = p->N;
   const int64_t total = p->buffered + n_in;
   const hipMemcpyKind kin = mem == PFB_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  {
+    // Carry without the concatenation copy: blocks whose rows start at or after the
+    // carried Bc rows read the new input in place (row shift Bc), the first ceil(Bc / keep)
+    // blocks a small stitched buffer; same blocks, same kernels as the concatenated run.
+    const int64_t Bc = p->buffered;
+    const int64_t B = synth_blocks(p, total);
+    const int64_t full = B * p->Lkeep;
+    int64_t input_idat = B * p->keep;
+    int64_t buffered = total - input_idat;
+    int64_t olen = full;
+    const int64_t rem = ((buffered % p->nu) + p->nu) % p->nu;
+    if (rem != 0) {
+      buffered += p->nu - rem;
+      input_idat = total - buffered;
+      olen = std::min(std::max<int64_t>(0, floordiv(input_idat * N * p->de, p->nu)), full);
+    }
+    if (input_idat < 0)
+      // no complete block and a carry rounded up past the data: InverseFilterBank.m:104-122
+      // would index input(:, :, input_idat + 1 : end) before the first sample (its rounding
+      // loop never settles); the call is rejected and the object state is left unchanged
+      return fail(PFB_ERR_INVALID_ARG,
+                  "InverseFilterBank: %lld buffered + %lld new rows hold no complete block and "
+                  "round the carry past the data (InverseFilterBank.m:104-122); pass more rows",
+                  (long long)Bc, (long long)n_in);
+    static const bool no_split = std::getenv("PFB_FB_NO_SPLIT") != nullptr;  // A/B
+    if (!no_split && mem == PFB_MEM_DEVICE && Bc > 0 && !p->has_spectral && input_idat >= Bc) {
+      if (n_out) *n_out = olen;
+      if (olen > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld",
+                                  (long long)cap, (long long)olen);
+      if (olen > 0) {
+        const int64_t b_s = std::min(B, (Bc + p->keep - 1) / p->keep);
+        if (b_s > 0) {
+          const int64_t L = std::min(total, (b_s - 1) * p->keep + p->Nf);
+          HIPCHK(p->work.ensure((size_t)p->n_pol * L * N * sizeof(float2)));
+          float2* wk = p->work.as<float2>();
+          HIPCHK(copy_pols(wk, L * N, p->carry.as<float2>(), Bc * N, std::min(Bc, L) * N, p->n_pol,
+                           hipMemcpyDeviceToDevice, s));
+          if (L > Bc)
+            HIPCHK(copy_pols(wk + Bc * N, L * N, (const float2*)in, in_ps, (L - Bc) * N, p->n_pol,
+                             hipMemcpyDeviceToDevice, s));
+          pfb_status st = synthesis_range(p, wk, L * N, 0, b_s, (float2*)out, out_ps, olen, s);
+          if (st != PFB_OK) return st;
+        }
+        pfb_status st = synthesis_range(p, (const float2*)in, in_ps, b_s, B, (float2*)out, out_ps, olen, s, Bc);
+        if (st != PFB_OK) return st;
+      }
+      if (buffered > 0) {
+        HIPCHK(p->carry.ensure((size_t)p->n_pol * buffered * N * sizeof(float2)));
+        HIPCHK(copy_pols(p->carry.as<float2>(), buffered * N, (const float2*)in + (input_idat - Bc) * N, in_ps,
+                         buffered * N, p->n_pol, hipMemcpyDeviceToDevice, s));
+      }
+      p->buffered = std::max<int64_t>(buffered, 0);
+      return PFB_OK;
+    }
+  }
   // input = cat(3, input_buffer, input); read in place when nothing is buffered
   const float2* w;
   int64_t wps;

@@ -157,6 +157,10 @@ struct LaunchEvents {
 };
 LaunchEvents& armed_launch_events();
 
+// device-to-device strided copy of n_pol rows (pfb_layout.hip)
+hipError_t launch_copy_rows(float2* dst, int64_t dps, const float2* src, int64_t sps, int64_t n, int n_pol,
+                            hipStream_t s);
+
 bool analysis_supported(int N, int P, int variant, bool* fused);
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s);
 bool chan_ifft_supported(int N);

@@ -263,6 +263,16 @@ __global__ void __launch_bounds__(TPB) copy_kernel(const float4* __restrict__ sr
     if (base + u * TPB < n4) dst[base + u * TPB] = v[u];
 }
 
+// n_pol rows of n samples, dst + q dps <- src + q sps (device to device): the strided
+// copies of the stream objects' carry buffers (hipMemcpy2D rejects row pitches of a few MB)
+__global__ void __launch_bounds__(TPB) copy_rows_kernel(float2* __restrict__ dst, int64_t dps,
+                                                        const float2* __restrict__ src, int64_t sps,
+                                                        int64_t n) {
+  const int64_t q = blockIdx.y;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB)
+    dst[q * dps + i] = src[q * sps + i];
+}
+
 unsigned grid_stride_blocks(int64_t total) {
   return (unsigned)std::min<int64_t>(std::max<int64_t>((total + TPB - 1) / TPB, 1), 4096);
 }
@@ -394,3 +404,13 @@ pfb_status pfb_device_copy(void* dst, const void* src, int64_t n_bytes, void* st
 }
 
 }  // extern "C"
+
+namespace pfb {
+hipError_t launch_copy_rows(float2* dst, int64_t dps, const float2* src, int64_t sps, int64_t n, int n_pol,
+                            hipStream_t s) {
+  if (n <= 0 || n_pol <= 0) return hipSuccess;
+  const unsigned gx = (unsigned)std::min<int64_t>(std::max<int64_t>((n + TPB - 1) / TPB, 1), 1024);
+  hipLaunchKernelGGL(copy_rows_kernel, dim3(gx, (unsigned)n_pol), dim3(TPB), 0, s, dst, dps, src, sps, n);
+  return hipGetLastError();
+}
+}  // namespace pfb

@@ -394,6 +394,39 @@ def test_inverse_filterbank_streaming_matches_oracle(gpu):
         assert ifb.buffered_samples == oifb.buffered_samples
 
 
+@pytest.mark.parametrize("N,nf,ov,chunks", [
+    (8, 128, 16, (500, 333, 1000, 20, 777)),
+    (256, 256, 48, (1000, 161, 5000, 3, 2222)),
+])
+def test_inverse_filterbank_stream_carry_in_place(gpu, N, nf, ov, chunks):
+    """Streaming InverseFilterBank on device tensors with carried rows: blocks that read
+    only the new input run on it in place (a row shift), the first ones on a small
+    stitched buffer (pfb_inverse_filterbank_execute); every chunk against the oracle."""
+    import torch
+    pfb = _pfb()
+    taps = _taps("test") if N == 8 else _taps("low87")
+    cfg = dict(filt_coeff=taps, channels=N, os_factor="8/7", input_fft_length=nf,
+               input_overlap=ov, deripple=True, temporal_taper="tukey")
+    ifb = pfb.InverseFilterBank(cfg)
+    oifb = orc.InverseFilterBankOracle(taps, N, "8/7", nf, ov, "tukey", deripple=True)
+    rng = np.random.default_rng(44)
+    for n in chunks:
+        x = _noise(rng, (2, N, n))
+        try:
+            ref = oifb.execute(x)
+        except ValueError:
+            # no complete block and the carry rounded past the data (InverseFilterBank.m:
+            # 104-122 indexes before the first sample): rejected, state unchanged
+            with pytest.raises(pfb.PfbError):
+                ifb.execute(torch.from_numpy(x).to(gpu))
+            continue
+        ifb, got = ifb.execute(torch.from_numpy(x).to(gpu))
+        assert tuple(got.shape) == ref.shape, (got.shape, ref.shape)
+        if ref.size:
+            assert_pfb_close(got.cpu().numpy(), ref, what=f"inverse stream N={N} chunk {n}")
+        assert ifb.buffered_samples == oifb.buffered_samples
+
+
 # ----------------------------------------------------------------------------- spectral taper
 # polyphase_synthesis.m:282 (FFFF = spectral_taper(FFFF, L, Ov)) through
 # InverseFilterBank.frequency_taper (InverseFilterBank.m:48-61); 'hann' on the L-vector
