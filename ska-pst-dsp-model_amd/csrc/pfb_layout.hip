@@ -168,11 +168,19 @@ __global__ void __launch_bounds__(TPB) moments_kernel(const float2* __restrict__
   const bool vec = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
   const int64_t n2 = vec ? n / 2 : 0;
   const int64_t stride = (int64_t)gridDim.x * TPB;
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n2; i += stride) {
-    const float4 v = reinterpret_cast<const float4*>(row)[i];
-    sr += (double)v.x + (double)v.z;
-    si += (double)v.y + (double)v.w;
-    s2 += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+  for (int64_t i0 = (int64_t)blockIdx.x * TPB + threadIdx.x; i0 < n2; i0 += 4 * stride) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)  // four loads in flight per thread
+      v[u] = i0 + u * stride < n2 ? reinterpret_cast<const float4*>(row)[i0 + u * stride]
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sr += (double)v[u].x + (double)v[u].z;
+      si += (double)v[u].y + (double)v[u].w;
+      s2 += (double)v[u].x * v[u].x + (double)v[u].y * v[u].y + (double)v[u].z * v[u].z +
+            (double)v[u].w * v[u].w;
+    }
   }
   for (int64_t i = 2 * n2 + (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += stride) {
     const float2 v = row[i];
@@ -222,7 +230,25 @@ __global__ void __launch_bounds__(TPB) quantize_kernel(const float2* __restrict_
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) stats[3] = scale;
   const float2* xr = x + blockIdx.y * ips;
   float2* yr = y + blockIdx.y * ops;
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+  const int64_t stride = (int64_t)gridDim.x * TPB;
+  // 16-byte loads and stores (two samples) when both rows are 16-B aligned; the loads of
+  // a thread's 4 iterations issue before its stores
+  const bool vec = ((reinterpret_cast<uintptr_t>(xr) | reinterpret_cast<uintptr_t>(yr)) & 15) == 0;
+  const int64_t n2 = vec ? n / 2 : 0;
+  const float4* x4 = reinterpret_cast<const float4*>(xr);
+  float4* y4 = reinterpret_cast<float4*>(yr);
+  for (int64_t i0 = (int64_t)blockIdx.x * TPB + threadIdx.x; i0 < n2; i0 += 4 * stride) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + u * stride < n2) v[u] = x4[i0 + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + u * stride < n2)
+        y4[i0 + u * stride] = make_float4(roundf(sf * v[u].x), roundf(sf * v[u].y), roundf(sf * v[u].z),
+                                          roundf(sf * v[u].w));
+  }
+  for (int64_t i = 2 * n2 + (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += stride) {
     const float2 v = xr[i];
     yr[i] = make_float2(roundf(sf * v.x), roundf(sf * v.y));
   }
@@ -377,7 +403,10 @@ pfb_status pfb_quantize(const pfb_cf32* in, int64_t in_pol_stride, int64_t n, in
   const dim3 g(std::max(1u, grid_stride_blocks(n * n_pol) / (unsigned)n_pol), (unsigned)n_pol);
   if (rms > 0) {
     LCHK(hipMemsetAsync(st, 0, 3 * sizeof(double), s));
-    hipLaunchKernelGGL(moments_kernel, g, TPB, 0, s, (const float2*)in, in_pol_stride, n, n_pol, st);
+    // few workgroups (each ends in three double atomics on one cache line, which serialise
+    // in L2): ~4 per CU in total, every thread streaming many 16-byte loads
+    const dim3 gm(std::max(1u, std::min(g.x, 1024u / (unsigned)n_pol)), (unsigned)n_pol);
+    hipLaunchKernelGGL(moments_kernel, gm, TPB, 0, s, (const float2*)in, in_pol_stride, n, n_pol, st);
     LCHK(hipGetLastError());
   }
   hipLaunchKernelGGL(quantize_kernel, g, TPB, 0, s, (const float2*)in, in_pol_stride, (float2*)out,
