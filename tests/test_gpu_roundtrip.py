@@ -204,6 +204,48 @@ def test_c2_full_size_linearity(c2):
     assert_pfb_close(lhs, rhs, tol=2e-6, scale=1.0, what="linearity (raw)")
 
 
+def test_c2_series_beyond_2gib(gpu):
+    """Maximum-size case: one 2^28 + 2^20 + 12345-sample series (over 2 GiB of input and
+    of output per polarisation, 2.4 GB of stage-1 rows) through the fused round trip, where every
+    kernel's per-workgroup buffer descriptor covers only its own range (kRsrcMaxBytes).
+    Blocks are local (rows b keep .. b keep + Nf, each row reading x[k M, k M + P N)), so
+    the first and the last blocks are checked against the oracle run on the matching
+    slices of the series (the tail slice starts on a commutator period, k0 a multiple of
+    nu, as the sharding helpers cut it)."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
+    n = (1 << 28) + (1 << 20) + 12345
+    g = torch.Generator(device=gpu).manual_seed(7)
+    xd = torch.complex(torch.randn((1, n), device=gpu, generator=g),
+                       torch.randn((1, n), device=gpu, generator=g)).to(torch.complex64) / np.sqrt(2.0)
+    ana = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
+    win = pfb.PFBWindow().lookup["tukey"](256, 48)
+    syn = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, 1, 0)
+    _, out = pfb.roundtrip(ana, syn, xd)
+    torch.cuda.synchronize()
+    M, PN, keep, lkeep = 224, 13 * 256, 160, 35840
+    K = (n - PN) // M
+    B = (K - 96) // keep
+    assert out.shape == (1, B * lkeep) and B * lkeep * 8 > (1 << 31)
+    dr = {"apply_deripple": 1, "filter_coeff": taps}
+    w = orc.pfb_window("tukey", 256, 48)
+
+    def ref_from(s0, s1):
+        xs = xd[:, s0:s1].cpu().numpy()[:, None, :]
+        chan = orc.polyphase_analysis(xs, taps, 256, "8/7")
+        return orc.polyphase_synthesis(chan, 1, 256, "8/7", dr, 1, 48, w)[:, 0, :]
+
+    head = ref_from(0, 1 << 21)
+    assert_pfb_close(out[:, :head.shape[1]].cpu().numpy(), head, scale=1.0, what="beyond 2 GiB: head")
+    b0 = B - 40
+    k0 = b0 * keep
+    assert k0 % 8 == 0
+    tail = ref_from(k0 * M, n)
+    assert tail.shape[1] == 40 * lkeep
+    assert_pfb_close(out[:, b0 * lkeep:].cpu().numpy(), tail, scale=1.0, what="beyond 2 GiB: tail")
+
+
 # ------------------------------------------------------------------ BASELINE C3 / C4 units
 def _np_noise(seed, n):
     rng = np.random.default_rng(seed)
