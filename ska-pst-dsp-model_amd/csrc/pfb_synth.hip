@@ -15,14 +15,11 @@ namespace pfb {
 // T4L: the workgroup's TG columns of the gain x twiddle table are copied to LDS once
 // and read from there every block (SKA-Mid: the 14.7 MB table was re-read from L2/MALL
 // for each of a workgroup's blocks; only where the copy keeps 4 workgroups per CU).
-// MODE: 0 = fused plan, 1 = split fused plan (SynthPlanSplit), 2 = split at 3 waves/SIMD.
 template <int NF, int W, int PAIRS, bool SPANS, bool PERSIST, int DK = 0, bool P16 = false,
-          bool T4L = false, int NTPW = NTP, int MODE = 0>
-__global__ __launch_bounds__(NTPW) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 3 : 2))) void synth_block_kernel(
-    SynthBlockArgs a) {
+          bool T4L = false, int NTPW = NTP>
+__global__ __launch_bounds__(NTPW) __attribute__((amdgpu_waves_per_eu(2))) void synth_block_kernel(SynthBlockArgs a) {
   using SS = SynthPairShape<NF, W, PAIRS>;
-  using SP = std::conditional_t<(MODE > 0), SynthPlanSplit<NF, W>, SynthPlan<NF, W>>;
-  static_assert(MODE == 0 || SP::split, "no split plan for this size");
+  using SP = SynthPlan<NF, W>;
   constexpr int R1 = synth_first_radix<NF, W>();
   constexpr int NB1 = NF / R1;
   constexpr int TG = 2 * PAIRS;
@@ -98,25 +95,18 @@ __global__ __launch_bounds__(NTPW) __attribute__((amdgpu_waves_per_eu(MODE == 2 
       stockham_pass_pair<NF, R1, 1, -1, PAIRS, NTPW>(in, rowsF, twF, tid);
       // the gain x twiddle loads go out BEFORE the next block's prefetch: vmcnt retires
       // in order, so waiting for them must not mean waiting for the HBM prefetch too
-      constexpr int RWF = SP::split ? RW1 / 2 : RW1;  // radix of the W transform's first pass
-      std::conditional_t<SP::split, v4f[RWF], v4f[PT][RW1]> t4;
-      if constexpr (SP::split) {
-        if constexpr (T4L) load_t4_lds_split<NBL, RWF, PAIRS, NTPW, SPANS>(t4, t4l, tid);
-        else load_t4_split<NBL, RWF, PAIRS, NTPW, SPANS>(t4, tw4r, N, tid);
-      } else {
-        if constexpr (T4L) load_t4_lds<NBL, RW1, PAIRS, NTPW>(t4, t4l, tid);
-        else load_t4<NBL, RW1, PAIRS, NTPW>(t4, tw4r, N, tid);
-      }
+      v4f t4[PT][RW1];
+      if constexpr (T4L) load_t4_lds<NBL, RW1, PAIRS, NTPW>(t4, t4l, tid);
+      else load_t4<NBL, RW1, PAIRS, NTPW>(t4, tw4r, N, tid);
       after_first();
       __syncthreads();
       if constexpr (!std::is_same_v<typename SP::Mid, Radices<>>) {
         run_fft_mid<NF, -1, PAIRS, NTPW, R1>(rowsF, twF, tid, typename SP::Mid{});
         __syncthreads();
       }
-      if constexpr (SP::split) fused_select_pass_split<NF, W, SP::RL, SPANS, PAIRS, NTPW>(rowsF, rowsW, twF, t4, tid);
-      else fused_select_pass<NF, W, SP::RL, SPANS, PAIRS, NTPW>(rowsF, rowsW, twF, t4, tid);
+      fused_select_pass<NF, W, SP::RL, SPANS, PAIRS, NTPW>(rowsF, rowsW, twF, t4, tid);
       __syncthreads();
-      run_fft_tail<W, +1, PAIRS, NTPW, RWF>(rowsW, out_for(b), twWl, tid, typename SP::Wrest{});
+      run_fft_tail<W, +1, PAIRS, NTPW, RW1>(rowsW, out_for(b), twWl, tid, typename SP::Wrest{});
     };
     if constexpr (!PERSIST) {
       __syncthreads();  // tables
@@ -156,12 +146,12 @@ __global__ __launch_bounds__(NTPW) __attribute__((amdgpu_waves_per_eu(MODE == 2 
   }
 }
 
-template <int NF, int W, int PAIRS, bool SPANS, int NTPW = NTP, int MODE = 0>
+template <int NF, int W, int PAIRS, bool SPANS, int NTPW = NTP>
 static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
   using SS = SynthPairShape<NF, W, PAIRS>;
   const int groups = a.N / (2 * PAIRS);
-  // workgroups per CU the registers allow at the kernel's 2 (MODE 2: 3) waves per SIMD
-  constexpr int vgpr_wgs = (MODE == 2 ? 12 : 8) * 64 / NTPW;
+  // workgroups per CU the registers allow at the kernel's 2 waves per SIMD
+  constexpr int vgpr_wgs = 8 * 64 / NTPW;
   if (a.ranges != 0 && SynthPlan<NF, W>::fused) {
     // persistent: block ranges so that ~LDS-limited workgroups per CU are resident;
     // the overlap-reuse instance when keep matches the compiled DK
@@ -177,10 +167,8 @@ static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
     static const bool no_t4l = std::getenv("PFB_SYNTH_NO_T4LDS") != nullptr;
     const bool t4l = T4 && !no_t4l && reuse && p16;
     const size_t lds = SS::lds_bytes + (t4l ? t4_bytes : 0);
-    // the split plan is compiled for the overlap-reuse, even-limit instances (C3); the
-    // others take the plain fused plan
-    auto kern = t4l ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true, T4, NTPW, MODE>
-              : reuse ? (p16 ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true, false, NTPW, MODE>
+    auto kern = t4l ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true, T4, NTPW>
+              : reuse ? (p16 ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true, false, NTPW>
                              : synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, false, false, NTPW>)
                       : (p16 ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, 0, true, false, NTPW>
                              : synth_block_kernel<NF, W, PAIRS, SPANS, FU, 0, false, false, NTPW>);
@@ -215,16 +203,6 @@ static hipError_t launch_sb_p(const SynthBlockArgs& a, hipStream_t s) {
   // (64 B of every stage-1 row instead of 32) and the per-workgroup tables are shared
   // by twice the threads (PFB_SYNTH_NTP=128 restores the 128-thread shape)
   static const int ntp_env = std::getenv("PFB_SYNTH_NTP") ? std::atoi(std::getenv("PFB_SYNTH_NTP")) : 0;
-  static const int pairs_env = std::getenv("PFB_SYNTH_PAIRS") ? std::atoi(std::getenv("PFB_SYNTH_PAIRS")) : 0;
-  if constexpr (NF == 512) {
-    // 8 pair rows (16 phases: whole 128-B lines of every stage-1 row; the fused pass
-    // busy on all 256 threads instead of half of them)
-    if (pairs_env == 8 && a.N % 16 == 0) return launch_sb<NF, W, 8, SPANS, 256>(a, s);
-    // split fused pass (PFB_SYNTH_SPLIT=1; 2: the same at 3 waves per SIMD)
-    static const int split_env = std::getenv("PFB_SYNTH_SPLIT") ? std::atoi(std::getenv("PFB_SYNTH_SPLIT")) : 0;
-    if (SPANS && a.N % 8 == 0 && split_env == 1) return launch_sb<NF, W, 4, SPANS, 256, 1>(a, s);
-    if (SPANS && a.N % 8 == 0 && split_env == 2) return launch_sb<NF, W, 4, SPANS, 256, 2>(a, s);
-  }
   if constexpr (NF >= 512) {
     constexpr int P2 = 256 / (NF / synth_first_radix<NF, W>());
     if (ntp_env != 128 && a.N % (2 * P2) == 0) return launch_sb<NF, W, P2, SPANS, 256>(a, s);

@@ -134,12 +134,10 @@ struct PairOut {
 template <int NF, int W>
 struct SynthPlan {
   static constexpr bool fused = false;
-  static constexpr bool split = false;
 };
 template <int R1_, class Mid_, int RL_, class Wrest_>
 struct FusedPlan {
   static constexpr bool fused = true;
-  static constexpr bool split = false;
   static constexpr int R1 = R1_;  // first Nf pass (loads from HBM)
   using Mid = Mid_;                // Nf passes between the first and the last
   static constexpr int RL = RL_;   // last Nf pass (fused with the selection)
@@ -151,22 +149,6 @@ template <> struct SynthPlan<128, 112> : FusedPlan<8, Radices<>, 16, Radices<8>>
 template <> struct SynthPlan<128, 96> : FusedPlan<8, Radices<>, 16, Radices<8>> {};
 template <> struct SynthPlan<512, 448> : FusedPlan<8, Radices<4>, 16, Radices<8, 4>> {};
 template <> struct SynthPlan<1024, 896> : FusedPlan<16, Radices<4>, 16, Radices<8, 8>> {};
-
-// Split fused plans: the fused pass runs on twice the threads.  Half h of the workgroup
-// computes the last Nf pass's outputs r = h (mod 2) by one decimation-in-frequency step
-// (radix 2, then radix RL/2); with the W-point transform's first radix RWS = W / (2 NBL)
-// the kept slots of one half (r'' of one parity) are exactly the inputs of one
-// radix-RWS butterfly (j + NBL e) of that transform, so selection, gain x twiddle and
-// the first W pass stay in registers and the pass needs no exchange between halves.
-// SKA-Mid: the unsplit fused pass keeps 128 of its 256 threads busy (4 pair rows x 32
-// butterflies), the split one all 256, at half the registers per thread.
-template <int R1_, class Mid_, int RL_, class Wrest_>
-struct SplitFusedPlan : FusedPlan<R1_, Mid_, RL_, Wrest_> {
-  static constexpr bool split = true;
-};
-template <int NF, int W>
-struct SynthPlanSplit : SynthPlan<NF, W> {};
-template <> struct SynthPlanSplit<512, 448> : SplitFusedPlan<8, Radices<4>, 16, Radices<8, 8>> {};
 
 // Overlap-reuse instance per transform size: DK = keep / (NF / R1) for the configured
 // overlap (SKA-Low Nf 256 / Ov 48: keep 160; 'test' Nf 128 / Ov 16: keep 96; SKA-Mid
@@ -262,80 +244,6 @@ __device__ __forceinline__ void fused_select_pass(const LdsPairs& rowsF, const L
       static_for<0, RW1>([&](auto rr) { rowsW.store(q, j * RW1 + rr, u[rr], p, rr); });
     }
   });
-}
-
-// ---------------------------------------------------------------- split fused pass
-// Thread tid: half h = tid / (PAIRS NBL) (wave-uniform), pair row q, butterfly j.
-// Half h holds the kept slots r'' = e + 2 r7 (r7 < RWS) with e = h (spans: slot parity =
-// bin parity) or 1 - h (critical: the half bands swap).
-template <int NF, int W, bool SPANS>
-__host__ __device__ constexpr int split_parity(int h) {
-  return SPANS ? h : 1 - h;
-}
-
-template <int NBL, int RWS, int PAIRS, int NTH, bool SPANS>
-__device__ __forceinline__ void load_t4_split(v4f (&t4)[RWS], __amdgpu_buffer_rsrc_t tr, int N, int tid) {
-  const int b = tid % (PAIRS * NBL);
-  const int e = SPANS ? tid / (PAIRS * NBL) : 1 - tid / (PAIRS * NBL);
-  const int q = b % PAIRS, j = b / PAIRS;
-  static_for<0, RWS>([&](auto r7) {
-    const int rr = e + 2 * r7;
-    const v4u x = __builtin_amdgcn_raw_buffer_load_b128(tr, ((j + NBL * rr) * N + 2 * q) * 8, 0, 0);
-    t4[r7] = __builtin_bit_cast(v4f, x);
-  });
-}
-
-template <int NBL, int RWS, int PAIRS, int NTH, bool SPANS>
-__device__ __forceinline__ void load_t4_lds_split(v4f (&t4)[RWS], const v4f* t4l, int tid) {
-  const int b = tid % (PAIRS * NBL);
-  const int e = SPANS ? tid / (PAIRS * NBL) : 1 - tid / (PAIRS * NBL);
-  const int q = b % PAIRS, j = b / PAIRS;
-  static_for<0, RWS>([&](auto r7) { t4[r7] = t4l[(j + NBL * (e + 2 * r7)) * PAIRS + q]; });
-}
-
-template <int NF, int W, int RL, bool SPANS, int HH>
-__device__ __forceinline__ void split_half(const cpx2 (&x)[RL], const v4f (&t4)[W / (2 * (NF / RL))],
-                                           const LdsPairs& rowsW, int q, int j) {
-  constexpr int NBL = NF / RL;
-  constexpr int RWS = W / (2 * NBL);
-  constexpr int H = RL / 2;
-  constexpr int E = split_parity<NF, W, SPANS>(HH);
-  // decimation in frequency: a[m] = X[2m + HH] after the radix-H DFT
-  cpx2 a[H];
-  static_for<0, H>([&](auto n) {
-    if constexpr (HH == 0) a[n] = cadd(x[n], x[n + H]);
-    else a[n] = ctw<decltype(n)::value, RL, -1>(csub(x[n], x[n + H]));
-  });
-  sdft<H, -1>(a);
-  cpx2 u[RWS];
-  static_for<0, RWS>([&](auto r7) {
-    constexpr int r = fused_src<NF, W, NBL, SPANS>(E + 2 * decltype(r7)::value);
-    static_assert(r % 2 == HH, "kept slot of the other half");
-    u[r7] = cmul(a[(r - HH) / 2], from_interleaved(t4[r7]));
-  });
-  sdft<RWS, +1>(u);
-  const int jw = j + NBL * E;  // butterfly of the W transform's first pass (NS = 1)
-  static_for<0, RWS>([&](auto r7) { rowsW.store(q, jw * RWS + r7, u[r7], r7, r7); });
-}
-
-template <int NF, int W, int RL, bool SPANS, int PAIRS, int NTH>
-__device__ __forceinline__ void fused_select_pass_split(const LdsPairs& rowsF, const LdsPairs& rowsW,
-                                                        const float2* __restrict__ twF,
-                                                        const v4f (&t4)[W / (2 * (NF / RL))], int tid) {
-  constexpr int NBL = NF / RL;
-  static_assert(2 * PAIRS * NBL == NTH, "split pass needs one butterfly half per thread");
-  static_assert((W / 2) % NBL == 0 && W % (2 * NBL) == 0 && RL % 2 == 0, "plan is not splittable");
-  const int b = tid % (PAIRS * NBL);
-  const int h = __builtin_amdgcn_readfirstlane(tid / (PAIRS * NBL));
-  const int q = b % PAIRS, j = b / PAIRS;
-  cpx2 x[RL];
-  static_for<0, RL>([&](auto r) { x[r] = rowsF.load(q, j + r * NBL, r, r); });
-  __syncthreads();
-  float2 w[RL];
-  twiddle_powers<RL, -1>(twF, j, w);
-  static_for<1, RL>([&](auto r) { x[r] = cmul(x[r], w[r]); });
-  if (h == 0) split_half<NF, W, RL, SPANS, 0>(x, t4, rowsW, q, j);
-  else split_half<NF, W, RL, SPANS, 1>(x, t4, rowsW, q, j);
 }
 
 }  // namespace pfb
