@@ -121,6 +121,26 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* plan, const pfb_cf32* in,
                                   int64_t* n_out, int32_t mem, void* stream);
 int64_t pfb_filterbank_buffered(const pfb_analysis_plan* plan);
 pfb_status pfb_filterbank_reset(pfb_analysis_plan* plan);
+/* Rows the next pfb_filterbank_execute of n_in samples returns (the nu-trimmed T_out of
+ * FilterBank.m:93-104 over the carried + new samples); -1 on a null plan. */
+int64_t pfb_filterbank_output_rows(const pfb_analysis_plan* plan, int64_t n_in);
+
+/* The same stream call writing the channelised product strided (device buffers only,
+ * streaming Bunton kernel: N = 256): bin c of row k of polarisation p goes to
+ * out[p * out_pol_stride + k * row_stride + j * chan_stride], j = c, or with sel_n > 0
+ * the cascade's channel chomp j = c < sel_split ? c : c - sel_shift (bins in
+ * [sel_split, sel_split + sel_shift) and j >= sel_n dropped).  Serves the two-stage
+ * cascade (TwoStageFilterBank.m:92-110): stage 1 written channel-major (row_stride 1,
+ * chan_stride = series length) is the per-channel input of stage 2 with no corner turn;
+ * stage 2 written with row_stride nch1*nch2, out_pol_stride nch2 and the chomp
+ * (sel_split nch2/2-1, sel_shift = dropped bins) is the assembled output of
+ * TwoStageFilterBank.m:102-105 with no gather.  PFB_ERR_UNSUPPORTED for other kernels. */
+pfb_status pfb_filterbank_execute_strided(pfb_analysis_plan* plan, const pfb_cf32* in,
+                                          int64_t in_pol_stride, int64_t n_in, pfb_cf32* out,
+                                          int64_t out_pol_stride, int64_t row_stride,
+                                          int64_t chan_stride, int32_t sel_split,
+                                          int32_t sel_shift, int32_t sel_n,
+                                          int64_t out_capacity, int64_t* n_out, void* stream);
 
 /* ---------------------------------------------------------------- synthesis */
 typedef struct pfb_synthesis_desc {

@@ -129,7 +129,14 @@ def twostage(torch, pfb, noise, reps):
     ms = timeit(torch, lambda: ts2.execute(xs), reps)
     emit("TwoStageFilterBank 256x256 (stream call)", ms, 16 * (1 + 8 / 7) * (1 << 24),
          msamples_per_s=round((1 << 24) / ms / 1e3, 1),
-         note="bytes: the two analyses' input+output, excluding the corner turn")
+         note="bytes: the two analyses' input+output; strided stores, no corner turn / gather")
+    ts3 = pfb.TwoStageFilterBank(cfg)
+    ts3.strided = False
+    ts3.execute(xs)
+    ms = timeit(torch, lambda: ts3.execute(xs), reps)
+    emit("TwoStageFilterBank 256x256 (corner turn + gather path)", ms, 16 * (1 + 8 / 7) * (1 << 24),
+         msamples_per_s=round((1 << 24) / ms / 1e3, 1),
+         note="bytes: the two analyses' input+output, excluding the corner turn and gather")
 
 
 def cpu_baselines(pfb):

@@ -188,7 +188,7 @@ struct StreamShape {
 // r = 192 k mod 256 is a multiple of 64, e^{-2 pi i f r / 256} = i^{k f}, exact), and
 // fftshift + the 216-channel selection is output channel c = (f - 148) mod 256 < 216,
 // scaled by 2^12 (LowCbfArgs::scale).  Leading pre-padding zeros via AnalysisArgs::pad.
-template <int N, int P, int NU, int DE, bool ZOUT, bool LCBF = false>
+template <int N, int P, int NU, int DE, bool ZOUT, bool LCBF = false, bool GS = false>
 __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
   using SH = StreamShape<N, P, NU, DE>;
   constexpr int M = SH::M, PE = SH::PE, QS = SH::QS, T = SH::T, NEW = SH::NEW, WIN = SH::WIN;
@@ -292,6 +292,10 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
     __syncthreads();
     if constexpr (LCBF) {
       const LcbfRowStore st = LcbfRowStore::rows(opol, k0, T, a.row0, a.K, a.lcbf_scale);
+      block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
+    } else if constexpr (GS) {
+      const StridedRowStore st = StridedRowStore::rows(opol, k0, T, a.row0, a.K, a.out_rs, a.out_cs,
+                                                       a.sel_split, a.sel_shift, a.sel_n, N, (float)N);
       block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
     } else {
       const BufRowStore st = BufRowStore::rows(opol, k0, T, a.row0, a.K, N, (float)N);
@@ -797,7 +801,9 @@ template <int N, int P, int NU, int DE, bool LCBF = false>
 static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
   using SH = StreamShape<N, P, NU, DE>;
   auto kern = LCBF ? analysis_stream_kernel<N, P, NU, DE, false, true>
-              : a.z ? analysis_stream_kernel<N, P, NU, DE, true> : analysis_stream_kernel<N, P, NU, DE, false>;
+              : a.z ? analysis_stream_kernel<N, P, NU, DE, true>
+              : a.out_rs > 0 ? analysis_stream_kernel<N, P, NU, DE, false, false, true>
+                             : analysis_stream_kernel<N, P, NU, DE, false>;
   hipError_t e = set_lds(kern, SH::lds_bytes);
   if (e != hipSuccess) return e;
   const int64_t q_lo = a.row0 / NU;

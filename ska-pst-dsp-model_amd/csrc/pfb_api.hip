@@ -215,10 +215,18 @@ struct pfb_analysis_plan {
 // variant's circular shift is modulo K_total).  `in`/`out` are the call's bases.
 // z (round trip only): also emit the synthesis stage-1 rows of rows >= z_row0 into
 // z[pol][k - z_row0][t0] (AnalysisArgs::z).
+// Strided channelised output of the streaming analysis kernel (AnalysisArgs::out_rs):
+// pfb_filterbank_execute_strided
+struct OutLayout {
+  int64_t rs, cs;
+  int32_t split, shift, nsel;
+};
+
 static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
                                float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
                                int64_t K_total, hipStream_t s, float2* z = nullptr,
-                               int64_t z_ps = 0, int64_t z_row0 = 0, int64_t pad = 0) {
+                               int64_t z_ps = 0, int64_t z_row0 = 0, int64_t pad = 0,
+                               const OutLayout* lay = nullptr) {
   if (K_end <= row0) return PFB_OK;
   if (p->variant == pfb::kLowCbf) {
     pfb::LowCbfArgs l{};
@@ -260,6 +268,13 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   a.twN = p->twN.as<float2>();
   a.zrev = p->zrev.p ? p->zrev.as<int>() : nullptr;
   a.pad = pad;  // `in` starts `pad` samples into the series (streaming kernel only)
+  if (lay) {
+    a.out_rs = (int)lay->rs;
+    a.out_cs = (int)lay->cs;
+    a.sel_split = lay->split;
+    a.sel_shift = lay->shift;
+    a.sel_n = lay->nsel;
+  }
   a.scratch = nullptr;
   if (!p->fused && !z) {
     HIPCHK(p->scratch.ensure((size_t)p->n_pol * (K_end - row0) * p->N * sizeof(float2)));
@@ -455,9 +470,46 @@ pfb_status pfb_analysis_execute(pfb_analysis_plan* p, const pfb_cf32* in, int64_
   return PFB_OK;
 }
 
+static pfb_status filterbank_exec(pfb_analysis_plan* p, const pfb_cf32* in, int64_t in_ps, int64_t n_in,
+                                  pfb_cf32* out, int64_t out_ps, int64_t cap, int64_t* n_out, int32_t mem,
+                                  void* stream, const OutLayout* lay);
+
 pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int64_t in_ps,
                                   int64_t n_in, pfb_cf32* out, int64_t out_ps, int64_t cap,
                                   int64_t* n_out, int32_t mem, void* stream) {
+  return filterbank_exec(p, in, in_ps, n_in, out, out_ps, cap, n_out, mem, stream, nullptr);
+}
+
+int64_t pfb_filterbank_output_rows(const pfb_analysis_plan* p, int64_t n_in) {
+  if (!p || n_in < 0) return -1;
+  const int64_t K = analysis_K(p, p->buffered + n_in);
+  return K - (K % p->nu);
+}
+
+pfb_status pfb_filterbank_execute_strided(pfb_analysis_plan* p, const pfb_cf32* in, int64_t in_ps,
+                                          int64_t n_in, pfb_cf32* out, int64_t out_ps,
+                                          int64_t row_stride, int64_t chan_stride, int32_t sel_split,
+                                          int32_t sel_shift, int32_t sel_n, int64_t cap,
+                                          int64_t* n_out, void* stream) {
+  if (!p || (!in && n_in > 0) || !out) return fail(PFB_ERR_INVALID_ARG, "null argument");
+  if (p->variant != pfb::kBunton || !analysis_offset_ok(p) || p->lowcbf_pad)
+    return fail(PFB_ERR_UNSUPPORTED, "strided output needs the streaming Bunton analysis kernel");
+  if (row_stride <= 0 || chan_stride <= 0 || sel_n < 0 || sel_split < 0 || sel_shift < 0 ||
+      (sel_n > 0 && sel_split + sel_shift > p->C) || sel_n > p->C)
+    return fail(PFB_ERR_INVALID_ARG, "bad strided output layout");
+  // one 16-row step's extent must fit a 32-bit buffer descriptor (StridedRowStore)
+  const int64_t jn = sel_n > 0 ? sel_n : p->C;
+  if ((64 * row_stride + jn * chan_stride + 1) * 8 > pfb::kRsrcMaxBytes)
+    return fail(PFB_ERR_UNSUPPORTED, "strided output extent exceeds a buffer descriptor");
+  const OutLayout lay{row_stride, chan_stride, sel_split, sel_shift, sel_n};
+  return filterbank_exec(p, in, in_ps, n_in, out, out_ps, cap, n_out, PFB_MEM_DEVICE, stream, &lay);
+}
+
+}  // extern "C"
+
+static pfb_status filterbank_exec(pfb_analysis_plan* p, const pfb_cf32* in, int64_t in_ps, int64_t n_in,
+                                  pfb_cf32* out, int64_t out_ps, int64_t cap, int64_t* n_out, int32_t mem,
+                                  void* stream, const OutLayout* lay) {
   if (!p || (!in && n_in > 0)) return fail(PFB_ERR_INVALID_ARG, "null argument");
   HIPCHK(hipSetDevice(p->device));
   hipStream_t s = (hipStream_t)stream;
@@ -487,12 +539,12 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
         float2* wk = p->work.as<float2>();
         HIPCHK(copy_pols(wk, L, p->carry.as<float2>(), B, std::min(B, L), p->n_pol, hipMemcpyDeviceToDevice, s));
         if (L > B) HIPCHK(copy_pols(wk + B, L, (const float2*)in, in_ps, L - B, p->n_pol, hipMemcpyDeviceToDevice, s));
-        pfb_status st = analysis_run(p, wk, L, L, (float2*)out, out_ps, 0, k_split, K, s);
+        pfb_status st = analysis_run(p, wk, L, L, (float2*)out, out_ps, 0, k_split, K, s, nullptr, 0, 0, 0, lay);
         if (st != PFB_OK) return st;
       }
       if (Kt > k_split) {
         pfb_status st = analysis_run(p, (const float2*)in, in_ps, n_in, (float2*)out, out_ps, k_split, Kt, K, s,
-                                     nullptr, 0, 0, B);
+                                     nullptr, 0, 0, B, lay);
         if (st != PFB_OK) return st;
       }
       // carry = input(:, :, input_idat + 1 : end): all of it lies in the new input
@@ -547,7 +599,8 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
         dps = Krun * p->C;
       }
     }
-    pfb_status st = analysis_run(p, w, wps, total, dst, dps, 0, Krun, K, s);
+    if (lay && dst != (float2*)out) return fail(PFB_ERR_UNSUPPORTED, "strided output through a staging buffer");
+    pfb_status st = analysis_run(p, w, wps, total, dst, dps, 0, Krun, K, s, nullptr, 0, 0, 0, lay);
     if (st != PFB_OK) return st;
     if (dst != (float2*)out) {
       const hipMemcpyKind ko = mem == PFB_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
@@ -567,6 +620,8 @@ pfb_status pfb_filterbank_execute(pfb_analysis_plan* p, const pfb_cf32* in, int6
   if (mem == PFB_MEM_HOST) HIPCHK(hipStreamSynchronize(s));
   return PFB_OK;
 }
+
+extern "C" {
 
 int64_t pfb_filterbank_buffered(const pfb_analysis_plan* p) { return p ? p->buffered : -1; }
 

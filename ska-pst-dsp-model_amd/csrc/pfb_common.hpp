@@ -62,6 +62,38 @@ struct BufRowStore {
 };
 
 
+// Rows [k0, k0 + T) of a strided channelised product (AnalysisArgs::out_rs): bin c of
+// row `row` at base + row * rs + j(c) * cs, valid rows [lo, hi) and kept bins only — the
+// rest are sent out of the descriptor's range (dropped).  Channel-major output (rs = 1,
+// cs = series length) is the per-channel series a cascade's second stage reads; rs =
+// nch1 nch2, cs = 1 with the chomp is TwoStageFilterBank's assembled output.
+struct StridedRowStore {
+  static constexpr bool kIsLds = false;
+  __amdgpu_buffer_rsrc_t r;
+  int lo, hi, rs, cs, split, shift, nsel;
+  float scale;
+  __device__ __forceinline__ void store(int row, int c, float2 v) const {
+    int j = c;
+    bool ok = row >= lo && row < hi;
+    if (nsel > 0) {
+      j = c < split ? c : c - shift;
+      ok = ok && (c < split || c >= split + shift) && j < nsel;
+    }
+    const uint32_t off = ok ? (uint32_t)((row * rs + j * cs) * 8) : 0xFFFFFFF0u;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v, scale)), r, off, 0, 0);
+  }
+  // the host checks that (T rs + jn cs) * 8 fits one descriptor (pfb_api.hip)
+  __device__ __forceinline__ static StridedRowStore rows(float2* base, int64_t k0, int T, int64_t k_lo,
+                                                          int64_t k_hi, int rs, int cs, int split,
+                                                          int shift, int nsel, int N, float scale) {
+    const int hi = (int)min(max(k_hi - k0, (int64_t)0), (int64_t)T);
+    const int lo = (int)min(max(k_lo - k0, (int64_t)0), (int64_t)T);
+    const int jn = nsel > 0 ? nsel : N;
+    const uint32_t bytes = hi > 0 ? (uint32_t)(((int64_t)(hi - 1) * rs + (int64_t)(jn - 1) * cs + 1) * 8) : 0u;
+    return StridedRowStore{make_rsrc(base + k0 * rs, bytes), lo, hi, rs, cs, split, shift, nsel, scale};
+  }
+};
+
 // LowCBF output rows (216 of the 256 FFT bins, fftshifted): bin f of row `row` is channel
 // c = (f - 148) mod 256 of output row k0 + row when c < 216 (polyphase_analysis_lowcbf.m /
 // PSTFilterbank.m:35-44); other bins and rows outside [k_lo, k_hi) are dropped by the

@@ -46,6 +46,12 @@ struct AnalysisArgs {
   // streaming kernel reads x[r N + c - pad] (zero for negative indices); 0 otherwise
   int64_t pad;
   float lcbf_scale;  // LowCBF streaming path: output scale (2^12)
+  // Strided channelised output (streaming kernel only, out_rs > 0): bin c of row k goes to
+  // out[pol][k * out_rs + j * out_cs] with j = c (sel_n = 0) or the two-stage chomp
+  // j = c < sel_split ? c : c - sel_shift, kept when c < sel_split or c >= sel_split +
+  // sel_shift, and j < sel_n (TwoStageFilterBank.m:102-105); out_rs = 0: [pol][k][c]
+  int out_rs, out_cs;
+  int sel_split, sel_shift, sel_n;
 };
 // SKA-Low CBF PST filterbank through the streaming analysis kernel (pfb_analysis.hip)
 hipError_t launch_lowcbf_stream(const AnalysisArgs& a, hipStream_t s);

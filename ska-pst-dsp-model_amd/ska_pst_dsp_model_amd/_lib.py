@@ -81,6 +81,10 @@ SYMBOLS = [
                                          c_int64, POINTER(c_int64), c_int32, c_void_p]),
     ("pfb_filterbank_buffered", c_int64, [c_void_p]),
     ("pfb_filterbank_reset", c_int32, [c_void_p]),
+    ("pfb_filterbank_output_rows", c_int64, [c_void_p, c_int64]),
+    ("pfb_filterbank_execute_strided", c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p,
+                                                 c_int64, c_int64, c_int64, c_int32, c_int32,
+                                                 c_int32, c_int64, POINTER(c_int64), c_void_p]),
     ("pfb_synthesis_plan_create", c_int32, [POINTER(SynthesisDesc), POINTER(c_void_p)]),
     ("pfb_synthesis_plan_destroy", c_int32, [c_void_p]),
     ("pfb_synthesis_output_length", c_int64, [c_void_p, c_int64]),

@@ -110,6 +110,28 @@ class AnalysisPlan:
     def reset(self):
         _lib.check(self._lib.pfb_filterbank_reset(self._h))
 
+    def stream_rows(self, n_in: int) -> int:
+        """Rows the next stateful execute of n_in samples returns (nu-trimmed)."""
+        return int(self._lib.pfb_filterbank_output_rows(self._h, int(n_in)))
+
+    def execute_strided(self, x, out, out_pol_stride: int, row_stride: int, chan_stride: int,
+                        sel=(0, 0, 0)):
+        """Stateful execute of device series ``x`` (n_pol, n_dat; any pol stride, unit
+        sample stride) writing bin c of row k of pol p to
+        ``out``'s storage at p * out_pol_stride + k * row_stride + j * chan_stride
+        (``pfb_filterbank_execute_strided``; sel = (split, shift, n) is the cascade's
+        channel chomp).  Returns the number of rows written."""
+        if x.shape[0] != self.n_pol or x.stride(1) != 1:
+            raise ValueError("execute_strided: (n_pol, n_dat) series with unit sample stride")
+        n_dat = int(x.shape[1])
+        rows = self.stream_rows(n_dat)
+        n_out = c_int64(0)
+        _lib.check(self._lib.pfb_filterbank_execute_strided(
+            self._h, c_void_p(x.data_ptr()), x.stride(0), n_dat, c_void_p(out.data_ptr()),
+            int(out_pol_stride), int(row_stride), int(chan_stride), int(sel[0]), int(sel[1]),
+            int(sel[2]), rows, byref(n_out), _stream_of(x)))
+        return int(n_out.value)
+
     def _prep_in(self, x):
         """-> (array (n_pol, n_dat) complex64 contiguous, is_device)."""
         if is_device_array(x):

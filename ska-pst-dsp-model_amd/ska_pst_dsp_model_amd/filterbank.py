@@ -208,10 +208,12 @@ class TwoStageFilterBank(Channelizer):
 
     The Matlab object runs nch1 independent FilterBank objects in a loop (:92-110).
     Here stage 2 is ONE batched plan whose "polarisations" are the nch1 stage-1
-    channels (each keeps its own carry-over, as the separate objects do): a corner
-    turn (``pfb_corner_turn``) makes the per-channel series, one analysis launch
-    channelises all of them, and one gather (``pfb_gather_channels``) assembles the
-    output with the oversampled channels chomped out (:102-105)."""
+    channels (each keeps its own carry-over, as the separate objects do).  Stage 1
+    writes its product channel-major, so pol 1's channels are the stage-2 series as
+    they lie, and the batched stage 2 writes the assembled output with the oversampled
+    channels chomped out (:102-105) straight from its FFT
+    (``pfb_filterbank_execute_strided``, streaming kernel shapes); other shapes take a
+    corner turn (``pfb_corner_turn``) and a gather (``pfb_gather_channels``)."""
 
     def __init__(self, config, device: int = 0):
         self.stage1 = FilterBank(config, device=device)
@@ -224,6 +226,9 @@ class TwoStageFilterBank(Channelizer):
         self.built = False
         self.stage2 = None
         self.device = device
+        # both stages through pfb_filterbank_execute_strided where the kernels allow it
+        # (no corner turn, no gather); False: the corner-turn / gather path
+        self.strided = True
 
     def set_stage2_config(self, config):
         self.config2 = config
@@ -237,19 +242,27 @@ class TwoStageFilterBank(Channelizer):
 
     def execute(self, input):  # noqa: A002
         x, host = _to_device(input, self.device)
-        _, out1 = self.stage1.execute(x)          # (n_pol, nch1, T1) view
         if not self.built:
             self.build()
+        view = self._execute_strided(x) if self.strided else None
+        if view is None:
+            _, out1 = self.stage1.execute(x)      # (n_pol, nch1, T1) view
+            nch1 = 1 if self.single == 1 else self.stage1.n_chan
+            # per-channel series of pol 1: (T1, nch1) rows -> (nch1, T1)
+            rows = out1[0].transpose(0, 1)[:, :nch1]  # (T1, nch1) view of the engine buffer
+            view = self._stage2(layout.corner_turn(rows), nch1)
+        return self, (_to_host(view) if host else view)
+
+    def _chomp(self):
+        """(nch2 kept per stage-2 bank, dropped-bin count) of :81-85,102-105."""
         os_ = self.stage1.os_factor
-        nch1 = self.stage1.n_chan
         nch2_orig = self.stage2.n_chan
         nch2 = (nch2_orig * os_.de) // os_.nu if self.critical else nch2_orig
-        offset = nch2_orig - nch2
-        if self.single == 1:
-            nch1 = 1
-        # per-channel series of pol 1: (T1, nch1) rows -> (nch1, T1)
-        rows = out1[0].transpose(0, 1)[:, :nch1]  # (T1, nch1) view of the engine buffer
-        series = layout.corner_turn(rows)         # (nch1, T1)
+        return nch2, nch2_orig - nch2
+
+    def _stage2(self, series, nch1):
+        """Stage 2 over the (nch1, T1) series, then one gather assembles the output."""
+        nch2, offset = self._chomp()
         _, tmp = self.stage2.execute(series)      # (nch1, nch2_orig, T2) view
         buf2 = tmp.transpose(1, 2)                # (nch1, T2, nch2_orig) engine buffer
         T2 = int(buf2.shape[1])
@@ -260,8 +273,46 @@ class TwoStageFilterBank(Channelizer):
                                in_row_stride=buf2.stride(1), n_rows=T2, n_sel=nch2,
                                split=nch2 // 2 - 1, shift=offset, out=out,
                                out_outer_stride=nch2, out_row_stride=nch1 * nch2)
-        view = out.transpose(1, 2)                # (1, nch1*nch2, T2)
-        return self, (_to_host(view) if host else view)
+        return out.transpose(1, 2)                # (1, nch1*nch2, T2)
+
+    def _execute_strided(self, x):
+        """Both stages through pfb_filterbank_execute_strided: stage 1 writes its product
+        channel-major, so pol 1's channels are already the stage-2 series (no corner
+        turn), and stage 2 writes the assembled, chomped output (no gather).  Same
+        kernels and arithmetic as the corner-turn / gather path (bit-identical).  None
+        when stage 1 cannot take this path (its plan state is then untouched); a stage 2
+        that cannot takes the gather path."""
+        from ._lib import PFB_ERR_UNSUPPORTED, PfbError
+        s1, s2 = self.stage1, self.stage2
+        if s1.rndInput or s1.rndOutput or s2.rndInput or s2.rndOutput:
+            return None
+        import torch
+        p1 = s1._ensure_plan(_npol(x))
+        xs, _ = p1._prep_in(x)
+        T1 = p1.stream_rows(int(xs.shape[1]))
+        nch1_all = p1.out_chan
+        T1c = max(T1, 1)
+        ser = torch.empty((p1.n_pol, nch1_all, T1c), dtype=torch.complex64, device=xs.device)
+        try:
+            T1 = p1.execute_strided(xs, ser, nch1_all * T1c, 1, T1c)
+        except PfbError as e:
+            if e.status == PFB_ERR_UNSUPPORTED:
+                return None
+            raise
+        nch1 = 1 if self.single == 1 else nch1_all
+        series = ser[0, :nch1, :T1]               # (nch1, T1), unit sample stride
+        nch2, offset = self._chomp()
+        p2 = s2._ensure_plan(nch1)
+        T2 = p2.stream_rows(T1)
+        out = torch.empty((1, max(T2, 1), nch1 * nch2), dtype=torch.complex64, device=xs.device)
+        try:
+            T2 = p2.execute_strided(series, out, nch2, nch1 * nch2, 1,
+                                    (nch2 // 2 - 1, offset, nch2))
+        except PfbError as e:
+            if e.status == PFB_ERR_UNSUPPORTED:
+                return self._stage2(series, nch1)
+            raise
+        return out[:, :T2, :].transpose(1, 2)     # (1, nch1*nch2, T2)
 
 
 class TwoStageInverseFilterBank(DeChannelizer):

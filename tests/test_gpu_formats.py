@@ -211,6 +211,48 @@ def test_two_stage_filterbank_matches_oracle(gpu, critical, single):
         assert_pfb_close(got, ref, what=f"two-stage n={n}")
 
 
+@pytest.mark.parametrize("os_", ["8/7", "4/3"])
+@pytest.mark.parametrize("critical,single", [(0, 0), (1, 0), (0, 1)])
+def test_two_stage_strided_matches_gather_path(gpu, os_, critical, single):
+    """256 x 256 cascade on the streaming kernel: stage 1 written channel-major and stage 2
+    written assembled and chomped (pfb_filterbank_execute_strided) equals the corner-turn /
+    gather path bit for bit, over calls with carry-over in both stages."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, os_, 12)
+    a = pfb.TwoStageFilterBank(_fb_cfg(taps, 256, os_))
+    b = pfb.TwoStageFilterBank(_fb_cfg(taps, 256, os_))
+    b.strided = False
+    for ts in (a, b):
+        ts.critical, ts.single = critical, single
+    rng = np.random.default_rng(31)
+    for n in (1_500_000, 700_001, 1_200_000):
+        x = torch.from_numpy(_noise(rng, (2, 1, n))).cuda()
+        _, ya = a.execute(x)
+        _, yb = b.execute(x)
+        assert ya.shape == yb.shape and ya.shape[2] > 0
+        assert torch.equal(ya, yb)
+
+
+def test_two_stage_strided_matches_oracle(gpu):
+    """The strided cascade (256 x 256, critical) against the oracle's nch1 separate
+    FilterBank objects (TwoStageFilterBank.m:92-110), two calls."""
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
+    ts = pfb.TwoStageFilterBank(_fb_cfg(taps, 256))
+    ts.critical = 1
+    ots = orc.TwoStageFilterBankOracle(orc.FilterBankOracle(taps, 256, "8/7"),
+                                       lambda: orc.FilterBankOracle(taps, 256, "8/7"),
+                                       critical=True, single=False)
+    rng = np.random.default_rng(32)
+    for n in (2_000_000, 1_000_000):  # stage 2 needs > 5 000 stage-1 rows for 8 of its own
+        x = _noise(rng, (1, 1, n))
+        ts, got = ts.execute(x)
+        ref = ots.execute(x)
+        assert got.shape == ref.shape and got.shape[2] > 0
+        assert_pfb_close(got, ref, what=f"two-stage 256x256 strided n={n}")
+
+
 @pytest.mark.parametrize("critical,combine", [(False, 1), (True, 1), (True, 2)])
 def test_two_stage_inverse_matches_oracle(gpu, critical, combine):
     pfb = _pfb()
