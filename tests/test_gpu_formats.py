@@ -234,6 +234,27 @@ def test_two_stage_strided_matches_gather_path(gpu, os_, critical, single):
         assert torch.equal(ya, yb)
 
 
+def test_filterbank_strided_rejects(gpu):
+    """pfb_filterbank_execute_strided: a kernel without strided stores (N = 8) is
+    PFB_ERR_UNSUPPORTED and a bad layout PFB_ERR_INVALID_ARG, both before any state
+    changes (the carry is untouched)."""
+    import torch
+    pfb = _pfb()
+    from ska_pst_dsp_model_amd._lib import PFB_ERR_INVALID_ARG, PFB_ERR_UNSUPPORTED, PfbError
+    x = torch.from_numpy(_noise(np.random.default_rng(33), (1, 50_000))).cuda()
+    small = pfb.AnalysisPlan(pfb.design_PFB_FIR_filter(8, "8/7", 10), 8, "8/7", "polyphase_analysis", 1, 0)
+    out = torch.empty((1, 8, 8000), dtype=torch.complex64, device=x.device)
+    with pytest.raises(PfbError) as e:
+        small.execute_strided(x, out, 8 * 8000, 1, 8000)
+    assert e.value.status == PFB_ERR_UNSUPPORTED and small.buffered_samples == 0
+    plan = pfb.AnalysisPlan(pfb.design_PFB_FIR_filter(256, "8/7", 12), 256, "8/7", "polyphase_analysis", 1, 0)
+    out = torch.empty((1, 256, 256), dtype=torch.complex64, device=x.device)
+    for rs, cs, sel in ((0, 1, (0, 0, 0)), (1, 256, (200, 100, 10)), (1, 256, (0, 0, 300))):
+        with pytest.raises(PfbError) as e:
+            plan.execute_strided(x, out, 256 * 256, rs, cs, sel)
+        assert e.value.status == PFB_ERR_INVALID_ARG and plan.buffered_samples == 0
+
+
 def test_two_stage_strided_matches_oracle(gpu):
     """The strided cascade (256 x 256, critical) against the oracle's nch1 separate
     FilterBank objects (TwoStageFilterBank.m:92-110), two calls."""
