@@ -176,13 +176,17 @@ static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
     if (e != hipSuccess) return e;
     const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(vgpr_wgs, (160 * 1024) / lds));
     // resident-capacity ranges; when that leaves more than 16 blocks per range (many
-    // phase groups per block row: SKA-Mid N / TG = 1024 gives one range of 72 blocks),
-    // ranges of 6 blocks instead (oversubscribed, evenly split): C3 1.59 -> 1.51 ms.
-    // C2 (64 ranges of ~7 blocks) keeps the capacity rule.
+    // phase groups per block row: SKA-Mid N / TG = 512 gives one range of 72 blocks),
+    // ranges of ~18 blocks instead (oversubscribed, evenly split: 4 rounds of resident
+    // workgroups).  Round 1 (no LDS table copy) chose 6 blocks: 1.59 -> 1.51 ms; with
+    // the per-workgroup table copy (T4L) longer ranges copy it less often — r02_v13 sweep
+    // of the C3 synthesis: 1 / 2 / 4 / 12 / 24 ranges = 515 / 496 / 492 / 526-537 / 593 us
+    // (profiles/r02_v13_c3_ranges_ab.txt).  C2 (64 ranges of ~7 blocks) keeps the
+    // capacity rule.
     int ranges = a.ranges;
     if (ranges <= 0) {
       ranges = std::max(1, cu_count() * per_cu / (groups * a.n_pol));
-      if (ranges * 16 < a.n_blocks) ranges = (a.n_blocks + 5) / 6;
+      if (ranges * 16 < a.n_blocks) ranges = (a.n_blocks + 17) / 18;
     }
     ranges = std::min(ranges, a.n_blocks);
     dim3 grid((unsigned)(groups * ranges), (unsigned)a.n_pol);
