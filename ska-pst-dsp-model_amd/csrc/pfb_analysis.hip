@@ -188,6 +188,17 @@ struct StreamShape {
 // r = 192 k mod 256 is a multiple of 64, e^{-2 pi i f r / 256} = i^{k f}, exact), and
 // fftshift + the 216-channel selection is output channel c = (f - 148) mod 256 < 216,
 // scaled by 2^12 (LowCbfArgs::scale).  Leading pre-padding zeros via AnalysisArgs::pad.
+// The last FFT pass's output staged channel-major in the LDS rows' space (channel c at
+// c * (T + 1), odd stride: conflict-light column writes and row-pair reads) for the
+// channel-major store of a strided launch (out_rs = 1).
+template <int T>
+struct ColMajorLds {
+  static constexpr bool kIsLds = true;
+  float2* b;
+  __device__ __forceinline__ void store(int row, int c, float2 v) const { b[c * (T + 1) + row] = v; }
+  __device__ __forceinline__ float2 load(int row, int c) const { return b[c * (T + 1) + row]; }
+};
+
 template <int N, int P, int NU, int DE, bool ZOUT, bool LCBF = false, bool GS = false>
 __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
   using SH = StreamShape<N, P, NU, DE>;
@@ -294,9 +305,36 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
       const LcbfRowStore st = LcbfRowStore::rows(opol, k0, T, a.row0, a.K, a.lcbf_scale);
       block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
     } else if constexpr (GS) {
-      const StridedRowStore st = StridedRowStore::rows(opol, k0, T, a.row0, a.K, a.out_rs, a.out_cs,
-                                                       a.sel_split, a.sel_shift, a.sel_n, N, (float)N);
-      block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
+      if (a.out_rs == 1 && a.sel_n == 0) {
+        // channel-major (a cascade's stage-2 series): the last pass lands in LDS by
+        // channel, then each 8-lane group writes one channel's T = 16 consecutive
+        // samples as 8 x 16 B (one 128-B run) instead of 16 scattered 8-B stores
+        static_assert(N * (T + 1) <= T * SH::RS, "channel-major staging exceeds the LDS rows");
+        const ColMajorLds<T> cm{smem};
+        block_fft<N, -1, T, NT>(rows, cm, rows, tw, c);
+        __syncthreads();
+        const int hi = (int)min(max(a.K - k0, (int64_t)0), (int64_t)T);
+        const int lo = (int)min(max(a.row0 - k0, (int64_t)0), (int64_t)T);
+        const __amdgpu_buffer_rsrc_t r =
+            make_rsrc(opol + k0, hi > 0 ? (uint32_t)(((int64_t)(N - 1) * a.out_cs + hi) * 8) : 0u);
+        static_for<0, (T / 2) * N / NT>([&](auto iv) {
+          const int idx = c + decltype(iv)::value * NT;
+          const int ch = idx / (T / 2), r0 = 2 * (idx % (T / 2));
+          const float2 v0 = cscale(cm.load(r0, ch), (float)N), v1 = cscale(cm.load(r0 + 1, ch), (float)N);
+          const uint32_t off = (uint32_t)((ch * a.out_cs + r0) * 8);
+          if (r0 >= lo && r0 + 1 < hi) {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{v0.x, v0.y, v1.x, v1.y}), r, off, 0, 0);
+          } else {
+            if (r0 >= lo && r0 < hi) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v0), r, off, 0, 0);
+            if (r0 + 1 >= lo && r0 + 1 < hi)
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v1), r, off + 8, 0, 0);
+          }
+        });
+      } else {
+        const StridedRowStore st = StridedRowStore::rows(opol, k0, T, a.row0, a.K, a.out_rs, a.out_cs,
+                                                         a.sel_split, a.sel_shift, a.sel_n, N, (float)N);
+        block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
+      }
     } else {
       const BufRowStore st = BufRowStore::rows(opol, k0, T, a.row0, a.K, N, (float)N);
       block_fft<N, -1, T, NT>(rows, st, rows, tw, c);

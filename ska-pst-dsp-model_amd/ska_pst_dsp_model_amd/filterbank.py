@@ -291,7 +291,7 @@ class TwoStageFilterBank(Channelizer):
         xs, _ = p1._prep_in(x)
         T1 = p1.stream_rows(int(xs.shape[1]))
         nch1_all = p1.out_chan
-        T1c = max(T1, 1)
+        T1c = max(16, (T1 + 15) // 16 * 16)  # 128-B aligned channel runs
         ser = torch.empty((p1.n_pol, nch1_all, T1c), dtype=torch.complex64, device=xs.device)
         try:
             T1 = p1.execute_strided(xs, ser, nch1_all * T1c, 1, T1c)
