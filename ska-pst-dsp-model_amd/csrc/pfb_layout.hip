@@ -104,11 +104,65 @@ __global__ void __launch_bounds__(TPB) dada_pack_kernel(const float2* __restrict
   }
 }
 
+// TFP order, complex samples, P = 1 or 2: element (t, c) = i of the file is the P x 2
+// values at i * P * 2 whatever C is (reshape_dada_data.m), so a thread takes 4 adjacent
+// i: one run of 8 P sizeof(T) bytes in (16 B for NBIT 8 dual-pol) as 16-byte loads, and
+// per polarisation 4 samples = 2 x 16-byte stores out (the generic kernel issues one
+// byte load per value and one 8-byte store per sample).  Needs 16-B aligned buffers
+// and an even pol stride (checked by the launcher).
+template <class T, int P>
+__global__ void __launch_bounds__(TPB) dada_unpack_tfp4_kernel(const T* __restrict__ in, int64_t n,
+                                                               float2* __restrict__ out, int64_t ops) {
+  constexpr int V = 4;
+  constexpr int NV = V * P * 2;                 // values per thread
+  constexpr int BYTES = NV * (int)sizeof(T);    // 8 P sizeof(T): a multiple of 8
+  const int64_t i0 = ((int64_t)blockIdx.x * TPB + threadIdx.x) * V;
+  if (i0 >= n) return;
+  T vals[NV];
+  if (i0 + V <= n) {
+    const char* src = reinterpret_cast<const char*>(in + i0 * P * 2);
+    if constexpr (BYTES % 16 == 0) {
+#pragma unroll
+      for (int k = 0; k < BYTES / 16; ++k) {
+        const uint4 w = reinterpret_cast<const uint4*>(src)[k];
+        __builtin_memcpy(reinterpret_cast<char*>(vals) + 16 * k, &w, 16);
+      }
+    } else {
+      const uint2 w = *reinterpret_cast<const uint2*>(src);
+      __builtin_memcpy(vals, &w, 8);
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      float4* o = reinterpret_cast<float4*>(out + p * ops + i0);
+#pragma unroll
+      for (int h = 0; h < V / 2; ++h) {
+        const int a = (2 * h) * P * 2 + 2 * p, b = (2 * h + 1) * P * 2 + 2 * p;
+        o[h] = make_float4((float)vals[a], (float)vals[a + 1], (float)vals[b], (float)vals[b + 1]);
+      }
+    }
+  } else {
+    for (int64_t i = i0; i < n; ++i)
+      for (int p = 0; p < P; ++p) {
+        const int64_t e = i * P + p;
+        out[p * ops + i] = make_float2((float)in[2 * e], (float)in[2 * e + 1]);
+      }
+  }
+}
+
 template <class T>
 hipError_t launch_unpack(const void* in, int ndim, bool lowcbf, int64_t n_dat, int C, int P,
                          float2* out, int64_t ops, hipStream_t s) {
   const unsigned g = blocks_for(n_dat * C);
   const T* src = static_cast<const T*>(in);
+  const bool aligned = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0) && (P == 1 || ops % 2 == 0);
+  // (NBIT 32/64 keep the generic kernel: its 4- and 8-byte value loads already coalesce)
+  if (sizeof(T) <= 2 && ndim == 2 && !lowcbf && aligned && (P == 1 || P == 2)) {
+    const int64_t n = n_dat * C;
+    const unsigned g4 = blocks_for((n + 3) / 4);
+    if (P == 2) hipLaunchKernelGGL((dada_unpack_tfp4_kernel<T, 2>), g4, TPB, 0, s, src, n, out, ops);
+    else hipLaunchKernelGGL((dada_unpack_tfp4_kernel<T, 1>), g4, TPB, 0, s, src, n, out, ops);
+    return hipGetLastError();
+  }
   if (ndim == 2) {
     if (lowcbf) hipLaunchKernelGGL((dada_unpack_kernel<T, 2, true>), g, TPB, 0, s, src, n_dat, C, P, out, ops);
     else hipLaunchKernelGGL((dada_unpack_kernel<T, 2, false>), g, TPB, 0, s, src, n_dat, C, P, out, ops);

@@ -40,7 +40,7 @@ def test_dada_unpack_matches_reshape(gpu, nbit, ndim, n_pol, n_chan):
     import torch
     from ska_pst_dsp_model_amd import layout
     rng = np.random.default_rng(nbit * 100 + n_chan)
-    n_dat = 1000
+    n_dat = 1000 + n_chan % 2  # odd channel counts: a ragged tail for the 4-sample fast path
     raw = _file_samples(rng, nbit, n_dat * n_chan * n_pol * ndim)
     got = layout.dada_unpack(torch.from_numpy(raw.view(np.uint8)).to(gpu), nbit, ndim, n_chan,
                              n_pol)
