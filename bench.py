@@ -203,17 +203,51 @@ def copy_rate(torch, dev, lib, n_bytes: int = 1 << 31, reps: int = 20):
     return round(2.0 * n_bytes / (ms * 1e-3) / 1e9, 1) if ok else None
 
 
-def pmc_traffic():
-    """HBM bytes per launch per kernel class from the committed PMC summary
-    (scripts/pmc_summary.py --json, FETCH_SIZE/WRITE_SIZE passes), if any."""
-    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
+
+
+def kernel_key(name):
+    """Kernel name as the PMC summary keys it: the demangled template-id without the
+    return type, namespace and parameter list ("synth_block_kernel<256, 224, ...>")."""
+    if not name:
         return None
-    try:
-        with open(p) as f:
-            return json.load(f)
-    except Exception:
-        return None
+    return name.split("(")[0].replace("void ", "").replace("pfb::", "").strip()
+
+
+def pmc_traffic(path=PMC_TRAFFIC):
+    """HBM bytes per launch, per workload and kernel, from the committed PMC summary
+    (scripts/pmc_summary.py --json, FETCH_SIZE/WRITE_SIZE passes over bench.py)."""
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        return json.load(f)
+
+
+def traffic_for(workload, kernel, traffic):
+    """(bytes, None) of the PMC record whose kernel IS the timed kernel, else (None, why)."""
+    key = kernel_key(kernel)
+    if key is None:
+        return None, "no kernel name recorded for the dominant kernel class"
+    rec = (traffic.get(workload) or {}).get(key)
+    if rec is None:
+        return None, f"profiles/pmc_traffic.json has no {workload} record for {key}"
+    return rec["bytes"], None
+
+
+# PFB_* variables that mean nothing to the release library but would change what an
+# experiments build times (A/B knobs, timing masks that drop loads/stores): refused
+ENV_ALLOWED = {"PFB_PARITY_LOG"}
+
+
+def pfb_env():
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("PFB_")}
+
+
+def check_env():
+    bad = sorted(k for k in pfb_env() if k not in ENV_ALLOWED)
+    if bad:
+        sys.exit(f"bench.py: refusing to run with {', '.join(bad)} set: the benchmark times the "
+                 f"release library with no A/B knob or timing mask (unset them)")
 
 
 def e2e_pcie(torch, dev, pfb, ana, syn, n_pol, n_dat, chan_buf, out_buf, steps, world, dist):
@@ -294,6 +328,7 @@ WORKLOAD_NAMES = {
 
 def main():
     args = parse()
+    check_env()
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -421,6 +456,9 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
     step = step_pipelined if args.roundtrip else step_serial
 
     lib = _lib.load()
+    if lib.pfb_build_flags() & 1:
+        sys.exit(f"bench.py: {_lib.LIB_PATH} is an experiments build (A/B knobs, timing masks); "
+                 f"benchmark the release library")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -462,7 +500,10 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
         ms, nl, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
         lib.pfb_profile_read(w, ctypes.byref(ms), ctypes.byref(nl), ctypes.byref(by))
         if nl.value:
-            kern[names[w]] = {"avg_ms": ms.value / nl.value, "launches": nl.value,
+            buf = ctypes.create_string_buffer(512)
+            lib.pfb_profile_kernel_name(w, buf, len(buf))
+            kern[names[w]] = {"kernel": buf.value.decode() or None,
+                              "avg_ms": ms.value / nl.value, "launches": nl.value,
                               "alg_bytes_per_launch": by.value / nl.value,
                               "ms_per_step": ms.value / args.steps}
 
@@ -486,11 +527,15 @@ def report(args, res, world, workload, n_pol, n_dat, all_seeds):
         achieved = kd["alg_bytes_per_launch"] / (kd["avg_ms"] * 1e-3) / 1e9
     else:
         dom, achieved = None, 0.0
-    traffic = pmc_traffic()
-    tkey = dom if n_pol == 1 else None  # the committed PMC numbers are for the C2 launch
-    roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": ((traffic or {}).get(tkey) or {}).get("bytes") if tkey else None}
+    kname = kern[dom].get("kernel") if dom else None
+    traffic, why = traffic_for(workload, kname, pmc_traffic()) if dom else (None, "no kernel timed")
+    if why and not args.stub_device:
+        print(f"bench.py: WARNING roofline.traffic unavailable: {why}", file=sys.stderr, flush=True)
+    roof = {"bound": "hbm", "kernel": kernel_key(kname) or dom, "kernel_class": dom,
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
+    if why:
+        roof["traffic_missing"] = why
     if res["copy_gbs"]:
         # the same achieved rate against the measured device-copy rate (not the peak)
         roof["copy_achievable"] = res["copy_gbs"]
@@ -525,6 +570,7 @@ def report(args, res, world, workload, n_pol, n_dat, all_seeds):
         "ms_per_step_with_kernel_events": round(res["el_prof"] / args.steps * 1e3, 4),
         "kernels": kern,
     }
+    out["pfb_env"] = pfb_env()
     if args.stub_device:
         out["stub_device"] = True
     if res["e2e"] is not None:

@@ -293,6 +293,15 @@ pfb_status pfb_device_copy(void* dst, const void* src, int64_t n_bytes, void* st
 pfb_status pfb_profile_enable(int32_t enable);
 pfb_status pfb_profile_read(int32_t which, double* total_ms, int64_t* launches, double* bytes);
 pfb_status pfb_profile_reset(void);
+/* Name of the kernel whose launches class `which` recorded (the last one, demangled as a
+ * kernel trace prints it, e.g. "void pfb::synth_block_kernel<256, 224, ...>(pfb::
+ * SynthBlockArgs)"); "" when the class recorded no single-kernel launch.  Writes at most
+ * `len` bytes including the terminating NUL. */
+pfb_status pfb_profile_kernel_name(int32_t which, char* buf, int64_t len);
+
+/* Build flags of the loaded library: bit 0 = experiments build (A/B knobs and timing
+ * masks read from PFB_* environment variables; never a release or benchmark library). */
+int32_t pfb_build_flags(void);
 
 #ifdef __cplusplus
 }

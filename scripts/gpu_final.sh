@@ -18,6 +18,12 @@ echo "e2e ok"
 rm -rf gpurun_out/pmc_*
 bash scripts/gpu_pmc.sh FETCH_SIZE WRITE_SIZE || exit $?
 mv gpurun_out/pmc_1 gpurun_out/pmc_c2_fetch && mv gpurun_out/pmc_2 gpurun_out/pmc_c2_write
+BENCH_ARGS="--workload c4" bash scripts/gpu_pmc.sh FETCH_SIZE WRITE_SIZE || exit $?
+mv gpurun_out/pmc_1 gpurun_out/pmc_c4_fetch && mv gpurun_out/pmc_2 gpurun_out/pmc_c4_write
+# roofline.traffic records (copied to profiles/pmc_traffic.json after the run)
+cp profiles/pmc_traffic.json gpurun_out/pmc_traffic.json
+python3 scripts/pmc_summary.py --json gpurun_out/pmc_traffic.json c2 gpurun_out/pmc_c2_fetch gpurun_out/pmc_c2_write > /dev/null
+python3 scripts/pmc_summary.py --json gpurun_out/pmc_traffic.json c4 gpurun_out/pmc_c4_fetch gpurun_out/pmc_c4_write > /dev/null
 PMC_PROG="scripts/bench_aux.py --only-mid --reps 2" bash scripts/gpu_pmc.sh FETCH_SIZE WRITE_SIZE || exit $?
 mv gpurun_out/pmc_1 gpurun_out/pmc_c3_fetch && mv gpurun_out/pmc_2 gpurun_out/pmc_c3_write
 echo "pmc ok"

@@ -33,29 +33,16 @@ def load(dirs):
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
-def bench_name(k):
-    """bench.py kernel class of a kernel name (pfb_profile_read classes)."""
-    if "analysis_stream" in k:
-        # the ZOUT instance (last template argument true) also runs the channel IFFT
-        return "analysis+chan_ifft" if k.rstrip(">").endswith("true") else "analysis"
-    for key, v in (("analysis_fused", "analysis"), ("fir_generic", "analysis_fir"),
-                   ("fir_lds", "analysis_fir"), ("fir_window", "analysis_fir"),
-                   ("row_fft", "synth_chan_ifft"), ("synth_block", "synth_block")):
-        if key in k:
-            return v
-    return k
-
-
 def traffic_json(res):
-    """Per bench kernel class: HBM bytes per launch (2 x FETCH_SIZE KiB + WRITE_SIZE KiB)."""
+    """Per kernel (bench.py's kernel_key form): HBM bytes per launch
+    (2 x FETCH_SIZE KiB + WRITE_SIZE KiB)."""
     out = {}
     for k, cs in res.items():
         if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
             continue
-        name = bench_name(k)
         rd = 2 * cs["FETCH_SIZE"] * 1024
         wr = cs["WRITE_SIZE"] * 1024
-        out[name] = {"kernel": k, "read_bytes": rd, "write_bytes": wr, "bytes": rd + wr}
+        out[k] = {"read_bytes": rd, "write_bytes": wr, "bytes": rd + wr}
     return out
 
 
@@ -63,11 +50,19 @@ if __name__ == "__main__":
     args = sys.argv[1:]
     js = None
     if args and args[0] == "--json":
-        js, args = args[1], args[2:]
+        # --json OUT WORKLOAD DIR...: merge this workload's records into OUT (bench.py
+        # looks the timed kernel up as OUT[workload][kernel])
+        js, workload, args = args[1], args[2], args[3:]
     res = load(args if args else ["."])
     if js:
+        try:
+            with open(js) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            doc = {}
+        doc[workload] = traffic_json(res)
         with open(js, "w") as f:
-            json.dump(traffic_json(res), f, indent=1)
+            json.dump(doc, f, indent=1, sort_keys=True)
     for k, cs in res.items():
         print(f"== {k}")
         for c in sorted(cs):

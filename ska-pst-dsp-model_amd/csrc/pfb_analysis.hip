@@ -226,7 +226,7 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
   // the launcher sizes the ranges so that a workgroup's rows span <= kRsrcMaxBytes
   // (launch_stream); the min() only bounds the series tail beyond the range
   uint32_t nbytes = (uint32_t)min(max(avail, (int64_t)0) * 8, kRsrcMaxBytes);
-  if (a.timing_mask & 1) nbytes = 0;
+  if (tmask(a.timing_mask) & 1) nbytes = 0;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(xpol + gb, nbytes);
   // rows past the last window of the range (the unconditional last prefetch) re-read the
   // last row instead: an L2 hit rather than HBM traffic nobody uses
@@ -719,7 +719,7 @@ static hipError_t launch_fir_lds_t(const AnalysisArgs& a, hipStream_t s) {
   const int chunks = a.N / SH::CW;
   const int64_t nq = (a.K + NU - 1) / NU - a.row0 / NU;
   static const int target = [] {
-    const char* v = std::getenv("PFB_FIR_LDS_WGS");
+    const char* v = knob("PFB_FIR_LDS_WGS");
     return v ? std::max(1, std::atoi(v)) : 2048;
   }();
   int64_t ranges = std::max<int64_t>(1, std::min<int64_t>(target / chunks, nq / (4 * SH::U)));
@@ -732,9 +732,9 @@ static hipError_t launch_fir_lds_t(const AnalysisArgs& a, hipStream_t s) {
   dim3 grid((unsigned)(chunks * ranges), (unsigned)a.n_pol);
   // padded round trip: shift the column chunks so the Z stores are line-aligned
   // (PFB_FIR_ZALIGN=0: unshifted, A/B)
-  static const bool no_zalign = std::getenv("PFB_FIR_ZALIGN") && std::atoi(std::getenv("PFB_FIR_ZALIGN")) == 0;
+  static const bool no_zalign = knob("PFB_FIR_ZALIGN") && std::atoi(knob("PFB_FIR_ZALIGN")) == 0;
   const int cs = (a.variant == kPadded && a.z && !no_zalign) ? a.N - 1 : 0;
-  static const int xcd = std::getenv("PFB_FIR_LDS_XCD") ? std::atoi(std::getenv("PFB_FIR_LDS_XCD")) : 1;
+  static const int xcd = knob("PFB_FIR_LDS_XCD") ? std::atoi(knob("PFB_FIR_LDS_XCD")) : 1;
   if (a.variant == kBunton)
     hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kBunton>), grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);
   else
@@ -747,14 +747,14 @@ static hipError_t launch_fir_window_t(const AnalysisArgs& a, hipStream_t s) {
   const int chunks = a.N / NT;
   const int base = chunks * a.nu * a.n_pol;
   static const int target = [] {
-    const char* v = std::getenv("PFB_FIR_BLOCKS");
+    const char* v = knob("PFB_FIR_BLOCKS");
     return v ? std::max(1, std::atoi(v)) : 4 * 1024;
   }();
   static const int rows = [] {
-    const char* v = std::getenv("PFB_FIR_ROWS");
+    const char* v = knob("PFB_FIR_ROWS");
     return v ? std::atoi(v) : 2;
   }();
-  static const bool no_map = std::getenv("PFB_FIR_NO_SLICE_MAP") != nullptr;
+  static const bool no_map = knob("PFB_FIR_NO_SLICE_MAP") != nullptr;
   const int slice_map = !no_map && a.M % NT == 0;
   int ranges = std::max(1, (target + base - 1) / base);
   // one range of residue s reads input samples [k_first M - (PW + 1) N, k_last M + PW N]:
@@ -788,7 +788,7 @@ template <int DE>
 static bool launch_fir_window_de(const AnalysisArgs& a, hipStream_t s, hipError_t* e) {
   if (a.P > 32 || a.P < DE) return false;
   // the LDS-shared form where NU divides the workgroup (8/7, 4/3); PFB_FIR_LDS=0: A/B
-  static const bool no_lds = std::getenv("PFB_FIR_LDS") && std::atoi(std::getenv("PFB_FIR_LDS")) == 0;
+  static const bool no_lds = knob("PFB_FIR_LDS") && std::atoi(knob("PFB_FIR_LDS")) == 0;
   if constexpr (DE == 7 || DE == 3) {
     constexpr int NU = DE == 7 ? 8 : 4;
     if (!no_lds && a.nu == NU && a.N % (NT / NU) == 0) {
@@ -808,7 +808,7 @@ static bool launch_fir_window_de(const AnalysisArgs& a, hipStream_t s, hipError_
 
 static bool fir_window_applies(const AnalysisArgs& a) {
   if (a.N % NT != 0 || (int64_t)a.M * a.nu % a.N != 0) return false;
-  if (std::getenv("PFB_FIR_NO_WINDOW")) return false;
+  if (knob("PFB_FIR_NO_WINDOW")) return false;
   const int de = (int)((int64_t)a.M * a.nu / a.N);
   return (de == 7 || de == 3 || de == 27) && a.P <= 32 && a.P >= de;
 }
@@ -851,7 +851,7 @@ static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
   // ranges amortise each workgroup's start-up window load; measured 4 % faster than 3
   // (PFB_ANA_WG_PER_CU overrides, A/B knob)
   int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / SH::lds_bytes));
-  static const int env_wpc = std::getenv("PFB_ANA_WG_PER_CU") ? std::atoi(std::getenv("PFB_ANA_WG_PER_CU")) : 0;
+  static const int env_wpc = knob("PFB_ANA_WG_PER_CU") ? std::atoi(knob("PFB_ANA_WG_PER_CU")) : 0;
   if (env_wpc > 0) per_cu = env_wpc;
   const int64_t per_pol = std::max<int64_t>(1, (per_cu * cu_count()) / a.n_pol);
   int64_t wgs = std::min<int64_t>(n_steps, per_pol);
@@ -907,13 +907,13 @@ bool analysis_supported(int N, int P, int variant, bool* fused) {
 }
 
 bool analysis_can_emit_z(const AnalysisArgs& a) {
-  if (stream_shape(a) && std::getenv("PFB_ANALYSIS_NO_STREAM") == nullptr) return true;
+  if (stream_shape(a) && knob("PFB_ANALYSIS_NO_STREAM") == nullptr) return true;
   bool fused = false;
   return analysis_supported(a.N, a.P, a.variant, &fused) && !fused && fir_window_applies(a);
 }
 
 bool analysis_takes_offset(const AnalysisArgs& a) {
-  return stream_shape(a) && std::getenv("PFB_ANALYSIS_NO_STREAM") == nullptr;
+  return stream_shape(a) && knob("PFB_ANALYSIS_NO_STREAM") == nullptr;
 }
 
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
@@ -922,9 +922,9 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
   if (a.z && !analysis_can_emit_z(a)) return hipErrorInvalidValue;
   bool fused = false;
   if (!analysis_supported(a.N, a.P, a.variant, &fused)) return hipErrorInvalidValue;
-  static const bool no_stream = std::getenv("PFB_ANALYSIS_NO_STREAM") != nullptr;
+  static const bool no_stream = knob("PFB_ANALYSIS_NO_STREAM") != nullptr;
   if (fused && stream_shape(a) && !no_stream) {
-    static const int mask = std::getenv("PFB_ANA_MASK") ? std::atoi(std::getenv("PFB_ANA_MASK")) : 0;
+    static const int mask = knob("PFB_ANA_MASK") ? std::atoi(knob("PFB_ANA_MASK")) : 0;
     AnalysisArgs b = a;
     b.timing_mask = mask;
     return launch_stream_any(b, s);

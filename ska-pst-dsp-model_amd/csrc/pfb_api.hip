@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cxxabi.h>
 #include <string>
 #include <vector>
 
@@ -93,6 +94,7 @@ struct Profiler {
   double total_ms[4] = {0, 0, 0, 0};  // 0 analysis, 1 chan IFFT, 2 block, 3 analysis + chan IFFT
   int64_t launches[4] = {0, 0, 0, 0};
   double bytes[4] = {0, 0, 0, 0};
+  std::string names[4];  // kernel of each class's last single-kernel launch (demangled)
   hipEvent_t get() {
     if (!pool.empty()) {
       hipEvent_t e = pool.back();
@@ -119,6 +121,16 @@ struct Profiler {
 };
 Profiler g_prof;
 thread_local pfb::LaunchEvents g_armed;
+thread_local const char* g_launched = nullptr;
+
+static std::string demangle(const char* name) {
+  if (!name) return std::string();
+  int st = 0;
+  char* d = abi::__cxa_demangle(name, nullptr, nullptr, &st);
+  std::string out = (st == 0 && d) ? std::string(d) : std::string(name);
+  std::free(d);
+  return out;
+}
 
 // Times the launch(es) issued while in scope.  single = true: exactly one kernel launch
 // goes through pfb::launch_kernel, which records the two events inside its own dispatch
@@ -135,7 +147,10 @@ struct ProfScope {
       a = g_prof.get();
       b = g_prof.get();
       if (a && b) {
-        if (single) pfb::armed_launch_events() = pfb::LaunchEvents{a, b};
+        if (single) {
+          pfb::armed_launch_events() = pfb::LaunchEvents{a, b};
+          pfb::launched_kernel_name() = nullptr;
+        }
         else (void)hipEventRecord(a, s);
       }
     }
@@ -150,6 +165,7 @@ struct ProfScope {
           g_prof.pool.push_back(b);
           return;
         }
+        if (pfb::launched_kernel_name()) g_prof.names[which] = demangle(pfb::launched_kernel_name());
       } else {
         (void)hipEventRecord(b, s);
       }
@@ -181,6 +197,7 @@ hipError_t copy_pols(float2* dst, int64_t dps, const float2* src, int64_t sps, i
 }  // namespace
 
 pfb::LaunchEvents& pfb::armed_launch_events() { return g_armed; }
+const char*& pfb::launched_kernel_name() { return g_launched; }
 
 // error channel shared with the other C-ABI translation units (pfb_layout.hip)
 pfb_status pfb_set_error(pfb_status s, const char* msg) { return fail(s, "%s", msg); }
@@ -200,7 +217,6 @@ struct pfb_analysis_plan {
   int64_t n_taps = 0;
   bool fused = false;
   DevBuf taps, twN, scratch;
-  DevBuf ftab;  // Bunton: F = [N zeros, taps, N zeros] for the round trip's recomputed rows
   DevBuf zrev;  // padded generic round trip: index reversal (N - i) mod N of the row FFT input
   // streaming (FilterBank.m:13-14 input_buffer / buffered_samples)
   DevBuf carry, work, stage_in, stage_out;
@@ -394,11 +410,6 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
   for (int64_t i = 0; i < d->n_taps; ++i) taps[(size_t)i] = (float)d->taps[i];  // cast(filt, 'single')
   hipError_t e = upload(p->taps, taps);
   if (e == hipSuccess) e = upload(p->twN, twiddles(p->N, -1));
-  if (e == hipSuccess && p->variant == pfb::kBunton) {
-    std::vector<float> f((size_t)(p->P + 2) * p->N, 0.f);
-    for (int64_t i = 0; i < d->n_taps; ++i) f[(size_t)(p->N + i)] = (float)d->taps[i];
-    e = upload(p->ftab, f);
-  }
   if (e == hipSuccess && !p->fused && p->variant == pfb::kPadded) {
     std::vector<int> rev((size_t)p->N);
     for (int i = 0; i < p->N; ++i) rev[(size_t)i] = (p->N - i) % p->N;
@@ -417,7 +428,6 @@ pfb_status pfb_analysis_plan_destroy(pfb_analysis_plan* p) {
   (void)hipSetDevice(p->device);
   p->taps.release();
   p->twN.release();
-  p->ftab.release();
   p->zrev.release();
   p->scratch.release();
   p->carry.release();
@@ -525,7 +535,7 @@ static pfb_status filterbank_exec(pfb_analysis_plan* p, const pfb_cf32* in, int6
     const int64_t K = analysis_K(p, total);
     const int64_t Kt = K - (K % p->nu);
     const int64_t input_idat = (Kt * p->N * p->de) / p->nu;
-    static const bool no_split = std::getenv("PFB_FB_NO_SPLIT") != nullptr;  // A/B
+    static const bool no_split = pfb::knob("PFB_FB_NO_SPLIT") != nullptr;  // A/B
     if (!no_split && mem == PFB_MEM_DEVICE && B > 0 && p->variant == pfb::kBunton && analysis_offset_ok(p) &&
         input_idat >= B && p->lowcbf_pad == false) {
       if (n_out) *n_out = Kt;
@@ -883,11 +893,11 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
 
   auto* p = new pfb_synthesis_plan();
   p->device = d->device;
-  if (const char* v = std::getenv("PFB_SYNTH_RANGES")) p->ranges = std::max(-1, std::atoi(v));
-  if (const char* v = std::getenv("PFB_TIMING_MASK")) p->timing_mask = std::atoi(v);
-  if (const char* v = std::getenv("PFB_SYNTH_NO_REUSE")) p->no_reuse = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PFB_SYNTH_XCD")) p->xcd = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PFB_RT_CHUNK_BLOCKS")) p->rt_chunk_blocks = std::max(1, std::atoi(v));
+  if (const char* v = pfb::knob("PFB_SYNTH_RANGES")) p->ranges = std::max(-1, std::atoi(v));
+  if (const char* v = pfb::knob("PFB_TIMING_MASK")) p->timing_mask = std::atoi(v);
+  if (const char* v = pfb::knob("PFB_SYNTH_NO_REUSE")) p->no_reuse = std::atoi(v) != 0;
+  if (const char* v = pfb::knob("PFB_SYNTH_XCD")) p->xcd = std::atoi(v) != 0;
+  if (const char* v = pfb::knob("PFB_RT_CHUNK_BLOCKS")) p->rt_chunk_blocks = std::max(1, std::atoi(v));
   p->N = N;
   p->nu = nu;
   p->de = de;
@@ -1142,7 +1152,7 @@ pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* p, const pfb_cf32*
                   "InverseFilterBank: %lld buffered + %lld new rows hold no complete block and "
                   "round the carry past the data (InverseFilterBank.m:104-122); pass more rows",
                   (long long)Bc, (long long)n_in);
-    static const bool no_split = std::getenv("PFB_FB_NO_SPLIT") != nullptr;  // A/B
+    static const bool no_split = pfb::knob("PFB_FB_NO_SPLIT") != nullptr;  // A/B
     if (!no_split && mem == PFB_MEM_DEVICE && Bc > 0 && !p->has_spectral && input_idat >= Bc) {
       if (n_out) *n_out = olen;
       if (olen > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld",
@@ -1280,56 +1290,6 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
   float2* y = (float2*)chan;
   if (B == 0) return analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s);
 
-  // Recomputed stage-1 rows (Bunton streaming shapes, launch_synth_fir): the analysis
-  // writes only the channelised product and the block kernel evaluates the FIR sums of
-  // its own columns from the input, so the rows never cross HBM (555 instead of 727 MB
-  // per C2 step).  The output is bit-identical to the fused path below.  Opt-in
-  // (PFB_RT_FIR=1, read per call): measured no faster than the fused path on C2 and 3 %
-  // slower on C4 — the FIR's tile reads cost the synthesis more LDS time than the rows'
-  // HBM traffic saves.
-  const bool rtfir = std::getenv("PFB_RT_FIR") && std::atoi(std::getenv("PFB_RT_FIR")) != 0;
-  if (rtfir && pa->variant == pfb::kBunton && analysis_emits_z(pa) && pa->ftab.p && ps->identity_perm &&
-      !ps->has_cgain && !ps->has_spectral && ps->chunk_blocks <= 0 && off % pa->nu == 0) {
-    pfb::SynthBlockArgs a = synth_args(ps, nullptr, 0, 0, B, (float2*)out, out_ps, olen);
-    a.x = x;
-    a.x_pol_stride = in_ps;
-    a.n_dat = n_dat;
-    a.fir_f = pa->ftab.as<float>();
-    a.fir_nu = pa->nu;
-    a.fir_de = pa->de;
-    a.fir_M = pa->M;
-    a.fir_P = pa->P;
-    a.fir_k0 = off;
-    if (pfb::synth_fir_supported(a)) {
-      // PFB_RT_FIR_CONC=1: the analysis on the plan's own stream, concurrent with the
-      // synthesis (fork/join through events; A/B measurement)
-      const bool conc = std::getenv("PFB_RT_FIR_CONC") && std::atoi(std::getenv("PFB_RT_FIR_CONC")) != 0;
-      hipStream_t sa = s;
-      if (conc) {
-        if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));
-        while (pa->events.size() < 2) {
-          hipEvent_t e;
-          HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-          pa->events.push_back(e);
-        }
-        HIPCHK(hipEventRecord(pa->events[0], s));
-        HIPCHK(hipStreamWaitEvent(pa->aux, pa->events[0], 0));
-        sa = pa->aux;
-      }
-      pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, sa);
-      if (st != PFB_OK) return st;
-      {
-        ProfScope ps_(2, (double)ps->n_pol * B * ((double)ps->keep * pa->M * 8.0 + ps->Lkeep * 8.0), s);
-        HIPCHK(pfb::launch_synth_fir(a, s));
-      }
-      if (conc) {
-        HIPCHK(hipEventRecord(pa->events[1], sa));
-        HIPCHK(hipStreamWaitEvent(s, pa->events[1], 0));
-      }
-      return PFB_OK;
-    }
-  }
-
   // Fused: the analysis kernel also writes the synthesis stage-1 rows (the channel IFFT
   // of every row it produces, taken as N^2 x its FIR sums before the FFT rather than from
   // the rounded channelised row — equal in exact arithmetic, so the output agrees with
@@ -1338,7 +1298,7 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
   // analysis kernel that can emit the rows, no combine permutation / per-channel gain,
   // and device memory for the rows (bounded at 16 GiB; an explicit chunk size, or a
   // larger call, takes the chunked pipeline below).
-  static const bool no_fuse = std::getenv("PFB_RT_NO_FUSE") != nullptr;
+  static const bool no_fuse = pfb::knob("PFB_RT_NO_FUSE") != nullptr;
   // (generic N > 256 path: Z holds all K rows — the row FFT makes the channelised product
   // from them — and the synthesis starts at row `off`; streaming kernel: K - off rows)
   const int64_t z0 = pa->fused ? off : 0;
@@ -1449,8 +1409,19 @@ pfb_status pfb_profile_reset(void) {
     g_prof.total_ms[i] = 0;
     g_prof.launches[i] = 0;
     g_prof.bytes[i] = 0;
+    g_prof.names[i].clear();
   }
   return PFB_OK;
 }
+pfb_status pfb_profile_kernel_name(int32_t which, char* buf, int64_t len) {
+  if (which < 0 || which > 3) return fail(PFB_ERR_INVALID_ARG, "which must be 0..3");
+  if (!buf || len <= 0) return fail(PFB_ERR_INVALID_ARG, "null or empty buffer");
+  const std::string& n = g_prof.names[which];
+  const size_t k = std::min<size_t>(n.size(), (size_t)len - 1);
+  std::memcpy(buf, n.data(), k);
+  buf[k] = 0;
+  return PFB_OK;
+}
+int32_t pfb_build_flags(void) { return pfb::kExperiments ? 1 : 0; }
 
 }  // extern "C"

@@ -284,6 +284,7 @@ inline hipError_t launch_kernel(K kern, dim3 grid, dim3 block, size_t lds, hipSt
   if (ev.start && ev.stop) {
     hipExtLaunchKernelGGL(kern, grid, block, (uint32_t)lds, s, ev.start, ev.stop, 0, args...);
     ev = LaunchEvents{};
+    launched_kernel_name() = hipKernelNameRefByPtr(reinterpret_cast<const void*>(kern), s);
   } else {
     hipLaunchKernelGGL(kern, grid, block, lds, s, args...);
   }

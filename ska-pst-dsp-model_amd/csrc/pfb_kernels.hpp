@@ -5,7 +5,23 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 namespace pfb {
+
+// Release builds carry no tuning or timing switches: the A/B knobs (PFB_* environment
+// variables read through knob()) and the timing masks that drop a kernel's loads or
+// stores exist only in the experiments build (make EXPERIMENTS=1 ->
+// lib/libpfb_hip_exp.so, compiled with -DPFB_EXPERIMENTS).  In a release build knob()
+// returns null and tmask() 0 at compile time, so no environment variable reaches a
+// code path that skips work.
+#ifdef PFB_EXPERIMENTS
+constexpr bool kExperiments = true;
+#else
+constexpr bool kExperiments = false;
+#endif
+inline const char* knob(const char* name) { return kExperiments ? std::getenv(name) : nullptr; }
+__host__ __device__ constexpr int tmask(int m) { return kExperiments ? m : 0; }
 
 enum Variant { kBunton = 0, kPadded = 1, kLowCbf = 2 };
 
@@ -97,19 +113,8 @@ struct SynthBlockArgs {
   int ranges;              // 0: one workgroup per block; -1 persistent auto; >0 persistent ranges
   int no_reuse;            // 1: re-read the 2 Ov overlap rows from HBM (PFB_SYNTH_NO_REUSE, A/B only)
   int xcd;                 // 1: XCD-aware workgroup -> (phase group, range) order (PFB_SYNTH_XCD)
-  int timing_mask;         // timing experiments only (PFB_TIMING_MASK): bit0 drop Z loads
-                           // (input loads in launch_synth_fir), bit1 drop output stores, bit2
-                           // drop tw4 loads; launch_synth_fir: bit3 no FIR arithmetic, bit4 no
-                           // input tile store (results invalid)
-  // Round trip with the stage-1 rows recomputed from the input (launch_synth_fir): Z row
-  // t = N^2 v_{k0 + t}, v_k the Bunton FIR sums of the streaming analysis
-  // (analysis_stream_kernel), evaluated from x instead of read from Z.
-  const float2* x;         // [pol][t] analysis input
-  int64_t x_pol_stride;
-  int64_t n_dat;
-  const float* fir_f;      // F = [N zeros, taps (P rows of N), N zeros], (P + 2) N floats
-  int fir_nu, fir_de, fir_M, fir_P;
-  int64_t fir_k0;          // channelised row of Z row 0 (a multiple of fir_nu)
+  int timing_mask;         // experiments build only (PFB_TIMING_MASK, results invalid): bit0
+                           // drop Z loads, bit1 drop output stores, bit2 drop tw4 loads
 };
 
 // Synthesis with a non-identity spectral taper (pfb_spectral.hip): blocks [b0, b0 + nb)
@@ -162,6 +167,8 @@ struct LaunchEvents {
   hipEvent_t start = nullptr, stop = nullptr;
 };
 LaunchEvents& armed_launch_events();
+// name of the last kernel launched through armed events (pfb_profile_kernel_name)
+const char*& launched_kernel_name();
 
 // device-to-device strided copy of n_pol rows (pfb_layout.hip)
 hipError_t launch_copy_rows(float2* dst, int64_t dps, const float2* src, int64_t sps, int64_t n, int n_pol,
@@ -173,8 +180,5 @@ bool chan_ifft_supported(int N);
 hipError_t launch_chan_ifft(const ChanIfftArgs& a, hipStream_t s);
 bool synth_block_supported(int Nf, int W);
 hipError_t launch_synth_block(const SynthBlockArgs& a, hipStream_t s);
-// synthesis stage 2 with the stage-1 rows recomputed from the analysis input (no Z)
-bool synth_fir_supported(const SynthBlockArgs& a);
-hipError_t launch_synth_fir(const SynthBlockArgs& a, hipStream_t s);
 
 }  // namespace pfb

@@ -127,7 +127,7 @@ hipError_t launch_lowcbf(const LowCbfArgs& a, hipStream_t s) {
   if (a.K <= 0) return hipSuccess;
   // streaming path (analysis_stream_kernel<256, 12, 4, 3, LCBF>): persistent workgroups,
   // each input sample loaded once; PFB_LOWCBF_STREAM=0 keeps the one-shot kernel below
-  static const bool one_shot = std::getenv("PFB_LOWCBF_STREAM") && std::atoi(std::getenv("PFB_LOWCBF_STREAM")) == 0;
+  static const bool one_shot = knob("PFB_LOWCBF_STREAM") && std::atoi(knob("PFB_LOWCBF_STREAM")) == 0;
   if (!one_shot) {
     AnalysisArgs b{};
     b.in = a.in;

@@ -14,7 +14,7 @@ static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s
   if constexpr (N == 4096) {
     // persistent workgroups (row_fft_persist_kernel) once there are several rows per
     // resident workgroup; PFB_ROWFFT_PERSIST=0: one workgroup per row (A/B)
-    static const bool off = std::getenv("PFB_ROWFFT_PERSIST") && std::atoi(std::getenv("PFB_ROWFFT_PERSIST")) == 0;
+    static const bool off = knob("PFB_ROWFFT_PERSIST") && std::atoi(knob("PFB_ROWFFT_PERSIST")) == 0;
     const size_t bytes = ((size_t)RowShape<N>::RS + tw_slots(N)) * sizeof(float2);
     const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / bytes);
     const int64_t wgs = (int64_t)cu_count() * per_cu;

@@ -52,8 +52,8 @@ __global__ __launch_bounds__(NTPW) __attribute__((amdgpu_waves_per_eu(2))) void 
   for (int j = tid; j < NF; j += NTPW) win[j] = a.window[j];
 
   const float2* zpol = a.Z + pol * a.z_pol_stride + t0;
-  const uint32_t zbytes = (a.timing_mask & 1) ? 0u : (uint32_t)((NF - 1) * N + TG) * 8u;
-  const uint32_t twbytes = (a.timing_mask & 4) ? 0u : (uint32_t)((W - 1) * N + TG) * 8u;
+  const uint32_t zbytes = (tmask(a.timing_mask) & 1) ? 0u : (uint32_t)((NF - 1) * N + TG) * 8u;
+  const uint32_t twbytes = (tmask(a.timing_mask) & 4) ? 0u : (uint32_t)((W - 1) * N + TG) * 8u;
   const __amdgpu_buffer_rsrc_t tw4r = make_rsrc(a.tw4 + t0, twbytes);
   v4f* t4l = reinterpret_cast<v4f*>(reinterpret_cast<char*>(smem) + SS::lds_bytes);
   if constexpr (T4L) {
@@ -70,7 +70,7 @@ __global__ __launch_bounds__(NTPW) __attribute__((amdgpu_waves_per_eu(2))) void 
     const int64_t ob = (a.block0 + b) * (int64_t)a.Lkeep;  // first kept output sample
     const int64_t avail = a.out_limit - ob;
     const int64_t nk =
-        (a.timing_mask & 2) ? 0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
+        (tmask(a.timing_mask) & 2) ? 0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
     return PairOut<P16>{make_rsrc(opol + ob, (uint32_t)nk * 8u),
                    make_rsrc(opol + ob + 1, (uint32_t)max((int64_t)0, nk - 1) * 8u), N, a.t1_lo, t0,
                    a.scale};
@@ -164,7 +164,7 @@ static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
     // limit): SKA-Mid 25.7 + 14 KB; not SKA-Low (38.5 + 28 KB)
     constexpr size_t t4_bytes = (size_t)W * PAIRS * 16;
     constexpr bool T4 = SS::lds_bytes + t4_bytes <= (160 * 1024) / vgpr_wgs;
-    static const bool no_t4l = std::getenv("PFB_SYNTH_NO_T4LDS") != nullptr;
+    static const bool no_t4l = knob("PFB_SYNTH_NO_T4LDS") != nullptr;
     const bool t4l = T4 && !no_t4l && reuse && p16;
     const size_t lds = SS::lds_bytes + (t4l ? t4_bytes : 0);
     auto kern = t4l ? synth_block_kernel<NF, W, PAIRS, SPANS, FU, DK, true, T4, NTPW>
@@ -206,7 +206,7 @@ static hipError_t launch_sb_p(const SynthBlockArgs& a, hipStream_t s) {
   // Nf >= 512 (SKA-Mid): 256-thread workgroups, so one workgroup reads 8 output phases
   // (64 B of every stage-1 row instead of 32) and the per-workgroup tables are shared
   // by twice the threads (PFB_SYNTH_NTP=128 restores the 128-thread shape)
-  static const int ntp_env = std::getenv("PFB_SYNTH_NTP") ? std::atoi(std::getenv("PFB_SYNTH_NTP")) : 0;
+  static const int ntp_env = knob("PFB_SYNTH_NTP") ? std::atoi(knob("PFB_SYNTH_NTP")) : 0;
   if constexpr (NF >= 512) {
     constexpr int P2 = 256 / (NF / synth_first_radix<NF, W>());
     if (ntp_env != 128 && a.N % (2 * P2) == 0) return launch_sb<NF, W, P2, SPANS, 256>(a, s);

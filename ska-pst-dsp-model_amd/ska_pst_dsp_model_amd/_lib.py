@@ -125,6 +125,8 @@ SYMBOLS = [
     ("pfb_profile_read", c_int32, [c_int32, POINTER(c_double), POINTER(c_int64),
                                    POINTER(c_double)]),
     ("pfb_profile_reset", c_int32, []),
+    ("pfb_profile_kernel_name", c_int32, [c_int32, c_char_p, c_int64]),
+    ("pfb_build_flags", c_int32, []),
 ]
 
 _lib = None

@@ -55,6 +55,14 @@ def assert_pfb_close(got, ref, tol=PARITY_TOL, scale="rms", what=""):
     s, emax, erms, _ = parity_stats(got, ref, scale)
     ok = np.isclose(got / s, ref / s, atol=tol, rtol=tol) if got.size else np.ones(1, bool)
     frac = float(ok.mean())
+    # isclose margin: max |got - ref| / (atol + rtol |ref|) on the scaled values (np.isclose
+    # passes a sample at <= 1; the margin says how close the worst sample came)
+    if got.size:
+        g = got.astype(np.complex128) / s
+        r = ref.astype(np.complex128) / s
+        margin = float((np.abs(g - r) / (tol + tol * np.abs(r))).max())
+    else:
+        margin = 0.0
     log = os.environ.get("PFB_PARITY_LOG")
     if log:
         import json
@@ -63,9 +71,9 @@ def assert_pfb_close(got, ref, tol=PARITY_TOL, scale="rms", what=""):
             f.write(json.dumps({"test": test, "what": what, "n": int(got.size),
                                 "scale": scale if isinstance(scale, str) else "raw",
                                 "scale_value": s, "tol": tol, "max_err": emax, "rms_err": erms,
-                                "isclose_frac": frac}) + "\n")
+                                "isclose_frac": frac, "margin": margin}) + "\n")
     assert frac == 1.0, (f"{what}: isclose({tol}) fraction {frac:.6f}; error / {scale} scale: "
-                         f"max {emax:.3e}, rms {erms:.3e}")
+                         f"max {emax:.3e}, rms {erms:.3e}, margin {margin:.3f}")
     return emax
 
 

@@ -83,3 +83,46 @@ def test_gpus_must_match_launcher_world():
              env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+def test_refuses_work_dropping_knobs():
+    """A PFB_* knob (here a timing mask that drops the kernels' loads in an experiments
+    build) makes the bench exit non-zero before anything is timed."""
+    r = _run(["--stub-device", "--no-cpu-baseline", "--steps", "1", "--warmup", "0"],
+             env={"PFB_TIMING_MASK": "1"})
+    assert r.returncode != 0
+    assert "PFB_TIMING_MASK" in (r.stderr + r.stdout)
+
+
+def test_env_is_recorded():
+    r = _run(["--stub-device", "--no-cpu-baseline", "--steps", "1", "--warmup", "0"],
+             env={"PFB_PARITY_LOG": "/dev/null"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _json_line(r.stdout)["pfb_env"] == {"PFB_PARITY_LOG": "/dev/null"}
+
+
+def _report(workload, kernels, n_pol):
+    class A:
+        steps, warmup, graph, roundtrip, stub_device = 10, 3, 1, 1, True
+    res = {"el": 1e-3, "el_prof": 1e-3, "kern": kernels, "copy_gbs": None, "e2e": None,
+           "taps": 3073, "K": 74883, "n_out": 16737280}
+    return bench.report(A, res, 1, workload, n_pol, 1 << 24, [[100]])
+
+
+def test_roofline_traffic_is_the_pmc_record_of_the_timed_kernel():
+    """roofline.traffic = the committed PMC bytes of the kernel the library names for the
+    dominant class (matched by kernel name, not by class), else null with the reason."""
+    traffic = bench.pmc_traffic()
+    assert "c2" in traffic and traffic["c2"], "profiles/pmc_traffic.json has no C2 records"
+    name, rec = max(traffic["c2"].items(), key=lambda kv: kv[1]["bytes"])
+    kern = {"analysis+chan_ifft": {"kernel": f"void pfb::{name}(pfb::AnalysisArgs)", "avg_ms": 0.09,
+                                   "launches": 10, "alg_bytes_per_launch": 2.8e8, "ms_per_step": 0.09},
+            "synth_block": {"kernel": "void pfb::other_kernel<1>(pfb::SynthBlockArgs)", "avg_ms": 0.05,
+                            "launches": 10, "alg_bytes_per_launch": 2.8e8, "ms_per_step": 0.05}}
+    roof = _report("c2", kern, 1)["roofline"]
+    assert roof["kernel"] == name and roof["traffic"] == rec["bytes"]
+    assert "traffic_missing" not in roof
+    # a kernel without a PMC record: null, and the reason is in the line
+    kern["analysis+chan_ifft"]["kernel"] = "void pfb::not_profiled<2>(pfb::AnalysisArgs)"
+    roof = _report("c2", kern, 1)["roofline"]
+    assert roof["traffic"] is None and "not_profiled<2>" in roof["traffic_missing"]

@@ -47,7 +47,7 @@ CASES = [
     # emits the synthesis stage-1 rows)
     (256, "4/3", 12, 256, 48, "polyphase_analysis", 2, 1 << 19, 0, 3),
     (256, "8/7", 11, 256, 48, "polyphase_analysis", 1, (1 << 19) + 777, 0, 2),
-    # sample offsets a multiple of nu (where PFB_RT_FIR=1 recomputes the rows)
+    # sample offsets a multiple of nu
     (256, "8/7", 12, 256, 48, "polyphase_analysis", 2, 1 << 19, 0, 9),
     (256, "4/3", 12, 256, 48, "polyphase_analysis", 2, 1 << 19, 0, 5),
     (256, "8/7", 11, 256, 48, "polyphase_analysis", 1, (1 << 19) + 777, 0, 1),
@@ -381,8 +381,8 @@ def test_c3_full_size_impulse_and_linearity(gpu):
 
 
 RECOMPUTE_CASES = [
-    # (os, taps/chan, n_pol, n_dat, sample_offset): every size where the synthesis
-    # recomputes its stage-1 rows from the input (Bunton, N 256, Nf 256 / Ov 48)
+    # (os, taps/chan, n_pol, n_dat, sample_offset): streaming-analysis shapes of the fused
+    # round trip (Bunton, N 256, Nf 256 / Ov 48)
     ("8/7", 12, 1, 1 << 20, 1),
     ("8/7", 12, 2, 1 << 19, 17),
     ("8/7", 11, 1, 300_000, 1),
@@ -394,12 +394,12 @@ RECOMPUTE_CASES = [
 
 
 @pytest.mark.parametrize("case", RECOMPUTE_CASES)
-def test_roundtrip_recomputed_rows_bit_identical(gpu, case, monkeypatch):
-    """The synthesis that evaluates the Bunton FIR sums of its own columns from the input
-    (launch_synth_fir: no stage-1 rows in HBM) gives exactly the output of the fused path
-    that reads them (the default; the analysis kernel writes N^2 v_k): same FMA order,
-    same power-of-two scaling — and the same channelised product.  (The recomputing
-    path is opt-in, PFB_RT_FIR=1: measured no faster)"""
+def test_roundtrip_fused_and_chunked_paths_agree(gpu, case):
+    """pfb_roundtrip_execute has two internal paths: the fused one (the analysis kernel
+    writes the synthesis stage-1 rows as N^2 x its FIR sums) and the chunked pipeline
+    (an explicit chunk size: separate analysis and synthesis kernels, bit-identical to the
+    separate calls).  The channelised product is bit-identical on both; the outputs agree
+    within the reference's 1e-6 (include/pfb_api.h)."""
     import torch
     pfb = _pfb()
     os_, tpc, n_pol, n_dat, so = case
@@ -408,13 +408,12 @@ def test_roundtrip_recomputed_rows_bit_identical(gpu, case, monkeypatch):
     ana = pfb.AnalysisPlan(taps, 256, os_, "polyphase_analysis", n_pol, 0)
     win = pfb.PFBWindow().lookup["tukey"](256, 48)
     syn = pfb.SynthesisPlan(256, os_, 256, 48, True, 1, True, taps, win, None, n_pol, 0)
-    monkeypatch.setenv("PFB_RT_FIR", "1")
-    chan_new, out_new = pfb.roundtrip(ana, syn, x, sample_offset=so)
+    chan_f, out_f = pfb.roundtrip(ana, syn, x, sample_offset=so)
     torch.cuda.synchronize()
-    monkeypatch.setenv("PFB_RT_FIR", "0")
-    chan_old, out_old = pfb.roundtrip(ana, syn, x, sample_offset=so)
+    syn.set_chunk_blocks(3)
+    chan_c, out_c = pfb.roundtrip(ana, syn, x, sample_offset=so)
     torch.cuda.synchronize()
-    assert out_new.shape == out_old.shape and out_new.shape[1] > 0
-    assert torch.equal(chan_new, chan_old)
-    assert torch.equal(out_new, out_old), (
-        f"max |diff| {float((out_new - out_old).abs().max()):.3e}")
+    assert out_f.shape == out_c.shape and out_f.shape[1] > 0
+    assert torch.equal(chan_f, chan_c)
+    assert_pfb_close(out_f.cpu().numpy(), out_c.cpu().numpy(), scale=1.0,
+                     what="fused vs chunked round trip (raw)")
