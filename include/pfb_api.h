@@ -134,7 +134,10 @@ int64_t pfb_filterbank_output_rows(const pfb_analysis_plan* plan, int64_t n_in);
  * chan_stride = series length) is the per-channel input of stage 2 with no corner turn;
  * stage 2 written with row_stride nch1*nch2, out_pol_stride nch2 and the chomp
  * (sel_split nch2/2-1, sel_shift = dropped bins) is the assembled output of
- * TwoStageFilterBank.m:102-105 with no gather.  PFB_ERR_UNSUPPORTED for other kernels. */
+ * TwoStageFilterBank.m:102-105 with no gather.  PFB_ERR_UNSUPPORTED for other kernels.
+ * out_capacity is the number of pfb_cf32 elements available from `out`: a call whose
+ * furthest written element ((n_pol-1) out_pol_stride + (rows-1) row_stride + (j_max)
+ * chan_stride) lies beyond it fails with PFB_ERR_BUFFER_TOO_SMALL and writes nothing. */
 pfb_status pfb_filterbank_execute_strided(pfb_analysis_plan* plan, const pfb_cf32* in,
                                           int64_t in_pol_stride, int64_t n_in, pfb_cf32* out,
                                           int64_t out_pol_stride, int64_t row_stride,

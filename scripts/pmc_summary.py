@@ -14,7 +14,7 @@ import sys
 
 
 def short(name):
-    for k in ("analysis_fused", "analysis_stream", "row_fft", "synth_block", "fir_generic", "fir_window",
+    for k in ("analysis_fused", "analysis_stream", "row_fft", "synth_block", "synth_wave", "fir_generic", "fir_window",
               "fir_lds", "spectral", "tile_transpose"):
         if k in name:
             return name.split("(")[0].replace("void pfb::", "")

@@ -199,7 +199,9 @@ struct ColMajorLds {
   __device__ __forceinline__ float2 load(int row, int c) const { return b[c * (T + 1) + row]; }
 };
 
-template <int N, int P, int NU, int DE, bool ZOUT, bool LCBF = false, bool GS = false>
+// ZOUT: 0 no stage-1 rows; 1 rows [row][c] (AnalysisArgs::z); 2 / 4: runs of ZOUT rows per
+// column (AnalysisArgs::zblk) for the synthesis wave kernel.
+template <int N, int P, int NU, int DE, int ZOUT, bool LCBF = false, bool GS = false>
 __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
   using SH = StreamShape<N, P, NU, DE>;
   constexpr int M = SH::M, PE = SH::PE, QS = SH::QS, T = SH::T, NEW = SH::NEW, WIN = SH::WIN;
@@ -291,13 +293,28 @@ __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
     // registers (no inverse FFT; N^2 is a power of two, so the scaling is exact).
     const BufRowStore zs = BufRowStore::rows(ZOUT ? zpol : opol, k0, T, max(a.row0, a.z_row0), a.K,
                                              N, (float)N * (float)N);
+    // ZOUT >= 2: the step's T = 16 rows of column c are 16 / ZOUT runs of this column, row
+    // k - z_row0 = ZB g + gi at z[pol][(g N + c) ZB + gi]; rows (2m, 2m+1) go out as one 16-B
+    // store once both are summed (the launcher guarantees that k0 - z_row0 is a multiple
+    // of 16; rows past K land in the buffer's padding)
+    const int64_t kz = k0 - a.z_row0;
+    const __amdgpu_buffer_rsrc_t zb =
+        make_rsrc(ZOUT >= 2 ? a.z + pol * a.z_pol_stride + max(kz, (int64_t)0) * N : opol,
+                  (ZOUT >= 2 && kz >= 0) ? (uint32_t)(N * T * 8) : 0u);
     static_for<0, NU>([&](auto sv) {
       constexpr int s = decltype(sv)::value;
       static_for<0, QS>([&](auto qv) {
         constexpr int qq = decltype(qv)::value;
         const float2 v = make_float2(acc[s][qq].x, acc[s][qq].y);
         rows.store(qq * NU + s, c, v);
-        if constexpr (ZOUT) zs.store(qq * NU + s, c, v);
+        if constexpr (ZOUT == 1) zs.store(qq * NU + s, c, v);
+        if constexpr (ZOUT >= 2 && (s & 1)) {
+          constexpr int r1 = qq * NU + s, r0 = r1 - 1;
+          constexpr float n2 = (float)N * (float)N;
+          const v2f a0 = acc[s - 1][qq] * n2, a1 = acc[s][qq] * n2;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{a0.x, a0.y, a1.x, a1.y}), zb,
+                                                 (uint32_t)((((r0 / ZOUT) * N + c) * ZOUT + r0 % ZOUT) * 8), 0, 0);
+        }
       });
     });
     __syncthreads();
@@ -838,10 +855,12 @@ static hipError_t launch_fused(const AnalysisArgs& a, hipStream_t s) {
 template <int N, int P, int NU, int DE, bool LCBF = false>
 static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
   using SH = StreamShape<N, P, NU, DE>;
-  auto kern = LCBF ? analysis_stream_kernel<N, P, NU, DE, false, true>
-              : a.z ? analysis_stream_kernel<N, P, NU, DE, true>
-              : a.out_rs > 0 ? analysis_stream_kernel<N, P, NU, DE, false, false, true>
-                             : analysis_stream_kernel<N, P, NU, DE, false>;
+  auto kern = LCBF ? analysis_stream_kernel<N, P, NU, DE, 0, true>
+              : a.z ? (a.zblk == 4   ? analysis_stream_kernel<N, P, NU, DE, 4>
+                       : a.zblk == 2 ? analysis_stream_kernel<N, P, NU, DE, 2>
+                                     : analysis_stream_kernel<N, P, NU, DE, 1>)
+              : a.out_rs > 0 ? analysis_stream_kernel<N, P, NU, DE, 0, false, true>
+                             : analysis_stream_kernel<N, P, NU, DE, 0>;
   hipError_t e = set_lds(kern, SH::lds_bytes);
   if (e != hipSuccess) return e;
   const int64_t q_lo = a.row0 / NU;
@@ -912,6 +931,10 @@ bool analysis_can_emit_z(const AnalysisArgs& a) {
   return analysis_supported(a.N, a.P, a.variant, &fused) && !fused && fir_window_applies(a);
 }
 
+bool analysis_can_emit_zblk(const AnalysisArgs& a) {
+  return stream_shape(a) && knob("PFB_ANALYSIS_NO_STREAM") == nullptr && StreamShape<256, 13, 8, 7>::T == 16;
+}
+
 bool analysis_takes_offset(const AnalysisArgs& a) {
   return stream_shape(a) && knob("PFB_ANALYSIS_NO_STREAM") == nullptr;
 }
@@ -920,6 +943,9 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
   if (a.K <= a.row0) return hipSuccess;
   if (a.pad != 0 && !analysis_takes_offset(a)) return hipErrorInvalidValue;
   if (a.z && !analysis_can_emit_z(a)) return hipErrorInvalidValue;
+  if (a.z && a.zblk > 1 &&
+      (!analysis_can_emit_zblk(a) || ((a.row0 - a.z_row0) % 16) != 0 || (a.zblk != 2 && a.zblk != 4)))
+    return hipErrorInvalidValue;
   bool fused = false;
   if (!analysis_supported(a.N, a.P, a.variant, &fused)) return hipErrorInvalidValue;
   static const bool no_stream = knob("PFB_ANALYSIS_NO_STREAM") != nullptr;

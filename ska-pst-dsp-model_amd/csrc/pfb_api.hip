@@ -242,7 +242,7 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
                                float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
                                int64_t K_total, hipStream_t s, float2* z = nullptr,
                                int64_t z_ps = 0, int64_t z_row0 = 0, int64_t pad = 0,
-                               const OutLayout* lay = nullptr) {
+                               const OutLayout* lay = nullptr, int zblk = 0) {
   if (K_end <= row0) return PFB_OK;
   if (p->variant == pfb::kLowCbf) {
     pfb::LowCbfArgs l{};
@@ -265,6 +265,7 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   a.z = z;
   a.z_pol_stride = z_ps;
   a.z_row0 = z_row0;
+  a.zblk = zblk;
   a.in = in;
   a.in_pol_stride = in_ps;
   a.n_dat = n_dat;
@@ -328,6 +329,16 @@ static bool analysis_emits_z(const pfb_analysis_plan* p) {
   a.P = p->P;
   a.nu = p->nu;
   return pfb::analysis_can_emit_z(a);  // streaming kernel (N = 256) or register-window FIR
+}
+
+static bool analysis_emits_zblk(const pfb_analysis_plan* p) {
+  pfb::AnalysisArgs a{};
+  a.variant = p->variant;
+  a.N = p->N;
+  a.M = p->M;
+  a.P = p->P;
+  a.nu = p->nu;
+  return pfb::analysis_can_emit_zblk(a);  // streaming kernel (N = 256)
 }
 
 static int64_t analysis_K(const pfb_analysis_plan* p, int64_t n_dat) {
@@ -511,8 +522,20 @@ pfb_status pfb_filterbank_execute_strided(pfb_analysis_plan* p, const pfb_cf32* 
   const int64_t jn = sel_n > 0 ? sel_n : p->C;
   if ((64 * row_stride + jn * chan_stride + 1) * 8 > pfb::kRsrcMaxBytes)
     return fail(PFB_ERR_UNSUPPORTED, "strided output extent exceeds a buffer descriptor");
+  // out_capacity counts pfb_cf32 elements from `out`: the furthest element this call writes
+  // must lie inside it (a wrong stride is rejected, not written past the buffer)
+  const int64_t Kt = pfb_filterbank_output_rows(p, n_in);
+  if (n_out) *n_out = Kt;
+  if (Kt > 0) {
+    const int64_t last = (int64_t)(p->n_pol - 1) * out_ps + (Kt - 1) * row_stride + (jn - 1) * chan_stride;
+    if (last >= cap)
+      return fail(PFB_ERR_BUFFER_TOO_SMALL,
+                  "strided output: element %lld is written but out_capacity is %lld elements",
+                  (long long)last, (long long)cap);
+  }
   const OutLayout lay{row_stride, chan_stride, sel_split, sel_shift, sel_n};
-  return filterbank_exec(p, in, in_ps, n_in, out, out_ps, cap, n_out, PFB_MEM_DEVICE, stream, &lay);
+  return filterbank_exec(p, in, in_ps, n_in, out, out_ps, std::max<int64_t>(Kt, 0), n_out, PFB_MEM_DEVICE,
+                         stream, &lay);
 }
 
 }  // extern "C"
@@ -659,7 +682,7 @@ struct pfb_synthesis_plan {
   bool identity_perm = true;
   bool has_cgain = false;
   bool has_spectral = false;  // non-identity spectral taper: pfb_spectral.hip path
-  DevBuf window, tw4, twN, twNf, twW, perm, cgain;
+  DevBuf window, tw4, tw4s, twN, twNf, twW, perm, cgain;
   DevBuf taper, gainj, sbuf0, sbuf1;  // spectral taper (L), deripple gains (W), scratch
   DevBuf Z, carry, work, stage_in, stage_out;
   int64_t buffered = 0;
@@ -681,7 +704,7 @@ static int64_t synth_blocks(const pfb_synthesis_plan* p, int64_t n_dat) {
 
 static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64_t z_ps, int64_t b0,
                                    int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
-                                   hipStream_t s);
+                                   hipStream_t s, int zblk = 0);
 
 // Blocks [b0, b0 + nb) with a spectral taper (pfb_spectral.hip): Matlab's order — per
 // channel FFT, stitch x taper, then the L-point IFFT as row FFTs — in sub-chunks whose
@@ -766,7 +789,7 @@ static pfb_status synthesis_chunk(pfb_synthesis_plan* p, const float2* in, int64
 // Block kernel over blocks [b0, b0 + nb); Z row 0 is channelised row b0 * keep.
 static pfb::SynthBlockArgs synth_args(const pfb_synthesis_plan* p, const float2* Z, int64_t z_ps,
                                       int64_t b0, int64_t nb, float2* out, int64_t out_ps,
-                                      int64_t out_limit) {
+                                      int64_t out_limit, int zblk = 0) {
   pfb::SynthBlockArgs a{};
   a.Z = Z;
   a.z_pol_stride = z_ps;
@@ -788,6 +811,7 @@ static pfb::SynthBlockArgs synth_args(const pfb_synthesis_plan* p, const float2*
   a.window = p->window.as<float>();
   a.spans = p->spans;
   a.tw4 = p->tw4.as<float2>();
+  a.tw4s = p->tw4s.as<float2>();
   a.twNf = p->twNf.as<float2>();
   a.twW = p->twW.as<float2>();
   a.out_limit = out_limit;
@@ -795,13 +819,14 @@ static pfb::SynthBlockArgs synth_args(const pfb_synthesis_plan* p, const float2*
   a.no_reuse = p->no_reuse;
   a.xcd = p->xcd;
   a.timing_mask = p->timing_mask;
+  a.zblk = zblk;
   return a;
 }
 
 static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64_t z_ps, int64_t b0,
                                    int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
-                                   hipStream_t s) {
-  const pfb::SynthBlockArgs a = synth_args(p, Z, z_ps, b0, nb, out, out_ps, out_limit);
+                                   hipStream_t s, int zblk) {
+  const pfb::SynthBlockArgs a = synth_args(p, Z, z_ps, b0, nb, out, out_ps, out_limit, zblk);
   {
     ProfScope ps(2, (double)p->n_pol * (nb * p->keep * p->N * 8.0 + nb * p->Lkeep * 8.0), s);
     HIPCHK(pfb::launch_synth_block(a, s));
@@ -1018,7 +1043,8 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
   }
   hipError_t e = upload(p->window, window);
   // four-step twiddle x deripple gain, laid out [j'][t0] (coalesced in the block kernel)
-  std::vector<float2> tw4((size_t)N * W);
+  std::vector<float2> tw4((size_t)N * W), tw4s((size_t)N * W);
+  const double oscale = (double)p->de / (double)p->nu / (double)p->L;
   for (int t0 = 0; t0 < N; ++t0) {
     for (int jp = 0; jp < W; ++jp) {
       int64_t m = ((int64_t)t0 * expo[(size_t)jp]) % p->L;
@@ -1027,9 +1053,12 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
       const double ang = 2.0 * M_PI * (double)m / (double)p->L;
       const double gj = gain[(size_t)jp];
       tw4[(size_t)jp * N + t0] = make_float2((float)(gj * std::cos(ang)), (float)(gj * std::sin(ang)));
+      tw4s[(size_t)jp * N + t0] =
+          make_float2((float)(oscale * gj * std::cos(ang)), (float)(oscale * gj * std::sin(ang)));
     }
   }
   if (e == hipSuccess) e = upload(p->tw4, tw4);
+  if (e == hipSuccess) e = upload(p->tw4s, tw4s);
   if (e == hipSuccess) e = upload(p->perm, perm);
   if (e == hipSuccess && !cgain.empty()) {
     e = upload(p->cgain, cgain);
@@ -1066,7 +1095,7 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
 pfb_status pfb_synthesis_plan_destroy(pfb_synthesis_plan* p) {
   if (!p) return PFB_OK;
   (void)hipSetDevice(p->device);
-  for (DevBuf* b : {&p->window, &p->tw4, &p->twN, &p->twNf, &p->twW, &p->perm, &p->cgain,
+  for (DevBuf* b : {&p->window, &p->tw4, &p->tw4s, &p->twN, &p->twNf, &p->twW, &p->perm, &p->cgain,
                     &p->taper, &p->gainj, &p->sbuf0, &p->sbuf1, &p->Z, &p->carry, &p->work,
                     &p->stage_in, &p->stage_out})
     b->release();
@@ -1303,15 +1332,36 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
   // from them — and the synthesis starts at row `off`; streaming kernel: K - off rows)
   const int64_t z0 = pa->fused ? off : 0;
   const int64_t zr = K - z0;
-  const size_t zbytes = (size_t)pa->n_pol * zr * pa->N * sizeof(float2);
-  if (!no_fuse && analysis_emits_z(pa) && ps->identity_perm && !ps->has_cgain && !ps->has_spectral &&
-      ps->chunk_blocks <= 0 && zbytes <= ((size_t)16 << 30)) {
-    HIPCHK(ps->Z.ensure((size_t)pa->n_pol * zr * pa->N * sizeof(float2)));
+  // Nf = 256 synthesis through the wave kernel: the streaming analysis writes the rows in
+  // the blocked layout it reads (16-row runs per phase; the series' rows from `off` on,
+  // which must start a run; rows rounded up to whole runs)
+  // (PFB_SYNTH_WAVE=0: the block kernel on rows; PFB_ZBLK: the run length, experiments build)
+  static const bool no_wave = pfb::knob("PFB_SYNTH_WAVE") && std::atoi(pfb::knob("PFB_SYNTH_WAVE")) == 0;
+  static const int zb_knob = pfb::knob("PFB_ZBLK") ? std::atoi(pfb::knob("PFB_ZBLK")) : 2;
+  int zblk = (!no_wave && analysis_emits_zblk(pa) && z0 == off && off % 16 == 0) ? zb_knob : 0;
+  if (zblk && !pfb::synth_wave_supported(synth_args(ps, nullptr, 0, 0, B, nullptr, 0, 0, zblk))) zblk = 0;
+  const int64_t zrows = zblk ? (zr + 15) / 16 * 16 : zr;
+  const size_t zbytes = (size_t)pa->n_pol * zrows * pa->N * sizeof(float2);
+  bool fuse = !no_fuse && analysis_emits_z(pa) && ps->identity_perm && !ps->has_cgain &&
+              !ps->has_spectral && ps->chunk_blocks <= 0 && zbytes <= ((size_t)16 << 30);
+  if (fuse) {
+    // the rows of the whole call stay resident; a device without room for them takes the
+    // chunked pipeline below (its scratch is one chunk's rows) instead of failing
+    const hipError_t ze = ps->Z.ensure(zbytes);
+    if (ze == hipErrorOutOfMemory) {
+      (void)hipGetLastError();
+      fuse = false;
+    } else if (ze != hipSuccess) {
+      return fail(PFB_ERR_HIP, "round trip stage-1 rows (%zu bytes): %s", zbytes, hipGetErrorString(ze));
+    }
+  }
+  if (fuse) {
     float2* Z = ps->Z.as<float2>();
-    pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zr * pa->N, z0);
+    pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0,
+                                 nullptr, zblk);
     if (st != PFB_OK) return st;
-    return synthesis_blocks(ps, Z + (off - z0) * pa->N, zr * pa->N, 0, B, (float2*)out, out_ps,
-                            olen, s);
+    return synthesis_blocks(ps, Z + (off - z0) * pa->N, zrows * pa->N, 0, B, (float2*)out, out_ps,
+                            olen, s, zblk);
   }
 
   if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));

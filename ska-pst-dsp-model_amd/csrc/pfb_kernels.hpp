@@ -68,11 +68,18 @@ struct AnalysisArgs {
   // sel_shift, and j < sel_n (TwoStageFilterBank.m:102-105); out_rs = 0: [pol][k][c]
   int out_rs, out_cs;
   int sel_split, sel_shift, sel_n;
+  // z in a grouped layout (streaming kernel, round trip into synth_wave_kernel): zblk = ZB
+  // in {2, 4, 16} puts row k - z_row0 = ZB g + gi of column c at z[pol][g][c][gi] — ZB
+  // consecutive rows of one column are one run; needs (row0 - z_row0) % 16 == 0
+  // (launch_analysis checks); 0 or 1: rows [row][c]
+  int zblk;
 };
 // SKA-Low CBF PST filterbank through the streaming analysis kernel (pfb_analysis.hip)
 hipError_t launch_lowcbf_stream(const AnalysisArgs& a, hipStream_t s);
 // analysis kernels that can also emit the synthesis stage-1 rows (see AnalysisArgs::z)
 bool analysis_can_emit_z(const AnalysisArgs& a);
+// analysis kernels that can emit the stage-1 rows in the blocked layout (AnalysisArgs::zblk)
+bool analysis_can_emit_zblk(const AnalysisArgs& a);
 // analysis shapes whose kernel reads with an input offset (AnalysisArgs::pad)
 bool analysis_takes_offset(const AnalysisArgs& a);
 
@@ -109,12 +116,14 @@ struct SynthBlockArgs {
   const float2* tw4;       // [j'][t0] = gain[j'] e^{+2 pi i t0 expo[j'] / L} (W x N)
   const float2* twNf;      // e^{-2 pi i m / Nf}
   const float2* twW;       // e^{-2 pi i m / W}
+  const float2* tw4s;      // tw4 x (de/nu) / L, rounded once (synth_wave_kernel)
   int64_t out_limit;       // samples per pol actually written (InverseFilterBank trim)
   int ranges;              // 0: one workgroup per block; -1 persistent auto; >0 persistent ranges
   int no_reuse;            // 1: re-read the 2 Ov overlap rows from HBM (PFB_SYNTH_NO_REUSE, A/B only)
   int xcd;                 // 1: XCD-aware workgroup -> (phase group, range) order (PFB_SYNTH_XCD)
   int timing_mask;         // experiments build only (PFB_TIMING_MASK, results invalid): bit0
                            // drop Z loads, bit1 drop output stores, bit2 drop tw4 loads
+  int zblk;                // Z layout of AnalysisArgs::zblk (0/1 rows, else ZB-row runs)
 };
 
 // Synthesis with a non-identity spectral taper (pfb_spectral.hip): blocks [b0, b0 + nb)
@@ -179,6 +188,10 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s);
 bool chan_ifft_supported(int N);
 hipError_t launch_chan_ifft(const ChanIfftArgs& a, hipStream_t s);
 bool synth_block_supported(int Nf, int W);
+// Nf = 256 synthesis with one output phase per 16 lanes and no barrier in the block loop
+// (pfb_synth_wave.hip); launch_synth_block takes it where it applies
+bool synth_wave_supported(const SynthBlockArgs& a);
+hipError_t launch_synth_wave(const SynthBlockArgs& a, hipStream_t s);
 hipError_t launch_synth_block(const SynthBlockArgs& a, hipStream_t s);
 
 }  // namespace pfb

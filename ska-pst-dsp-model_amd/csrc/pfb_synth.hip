@@ -236,6 +236,8 @@ bool synth_block_supported(int Nf, int W) {
 
 hipError_t launch_synth_block(const SynthBlockArgs& a, hipStream_t s) {
   if (a.n_blocks <= 0) return hipSuccess;
+  // stage-1 rows for the wave kernel (the fused round trip, Nf = 256: zblk = run length)
+  if (a.zblk) return launch_synth_wave(a, s);
 #define X(a_, b_) \
   if (a.Nf == a_ && a.W == b_)  \
     return a.spans ? launch_sb_p<a_, b_, true>(a, s) : launch_sb_p<a_, b_, false>(a, s);

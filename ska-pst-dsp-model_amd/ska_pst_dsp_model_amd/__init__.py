@@ -17,6 +17,7 @@ from .filterbank import (Channelizer, DeChannelizer, FilterBank, InverseFilterBa
 from .firio import (design_PFB_FIR_filter, design_PFB_FIR_filter_two_stage,
                     read_fir_filter_coeff)
 from .window import PFBWindow, identity_taper
+from .streaming import Impulse, PureTone, TestImpulse, TestPureTone, sgcht
 from . import dada, harness, layout, sharding, verify
 
 __all__ = [
@@ -25,4 +26,5 @@ __all__ = [
     "Channelizer", "DeChannelizer", "FilterBank", "InverseFilterBank", "TwoStageFilterBank",
     "TwoStageInverseFilterBank", "design_PFB_FIR_filter", "design_PFB_FIR_filter_two_stage",
     "read_fir_filter_coeff", "PFBWindow", "identity_taper", "roundtrip", "calc_output_nbins",
+    "sgcht", "PureTone", "Impulse", "TestPureTone", "TestImpulse",
 ]

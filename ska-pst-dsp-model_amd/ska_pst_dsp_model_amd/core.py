@@ -124,12 +124,14 @@ class AnalysisPlan:
         if x.shape[0] != self.n_pol or x.stride(1) != 1:
             raise ValueError("execute_strided: (n_pol, n_dat) series with unit sample stride")
         n_dat = int(x.shape[1])
-        rows = self.stream_rows(n_dat)
+        # elements of out's storage from its first element (the C ABI range-checks the
+        # furthest strided write against it)
+        cap = out.untyped_storage().nbytes() // out.element_size() - out.storage_offset()
         n_out = c_int64(0)
         _lib.check(self._lib.pfb_filterbank_execute_strided(
             self._h, c_void_p(x.data_ptr()), x.stride(0), n_dat, c_void_p(out.data_ptr()),
             int(out_pol_stride), int(row_stride), int(chan_stride), int(sel[0]), int(sel[1]),
-            int(sel[2]), rows, byref(n_out), _stream_of(x)))
+            int(sel[2]), int(cap), byref(n_out), _stream_of(x)))
         return int(n_out.value)
 
     def _prep_in(self, x):

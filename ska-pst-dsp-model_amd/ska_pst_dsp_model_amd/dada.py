@@ -17,6 +17,7 @@ same.
 from __future__ import annotations
 
 import os
+import re
 
 import numpy as np
 
@@ -34,12 +35,20 @@ def _torch():
 
 
 # ------------------------------------------------------------------ header
+_WS = re.compile(r"[ \f\n\r\t\v]+")
+
+
 def _parse_header(text: str) -> dict:
+    """read_header.m:16-27: lines split at '\n'; '#' lines skipped; strsplit(line) at
+    collapsed whitespace (a leading or trailing run gives an empty first or last token, as
+    in Matlab); a line with more than one token maps token 1 -> token 2.  The text ends at
+    the first NUL (the header padding; read_header.m would store that padding under an
+    empty key)."""
     hdr = {}
     for line in text.split("\n"):
         if line.startswith("#"):
             continue
-        tok = line.split()  # strsplit(line): whitespace, collapsed
+        tok = _WS.split(line)
         if len(tok) > 1:
             hdr[tok[0]] = tok[1]
     return hdr

@@ -152,3 +152,48 @@ def test_c5_scoring_matches_reference_on_oracle():
             assert r["max_spurious_dB"] <= -60.0, r
             scored += 1
     assert scored >= 8
+
+
+# ------------------------------------------------------------------ sgcht testers
+def test_sgcht_generators_carry_state():
+    """PureTone.m / Impulse.m: the phase (and the delta position) continue across calls."""
+    from ska_pst_dsp_model_amd import streaming as sgcht
+    g = sgcht.PureTone(frequency=0.25)
+    _, a = g.generate(6)
+    _, b = g.generate(6)
+    whole = sgcht.PureTone(frequency=0.25).generate(12)[1]
+    assert np.array_equal(np.concatenate([a, b], axis=2), whole)
+    imp = sgcht.Impulse(offset=7, noise=0.0)
+    _, x1 = imp.generate(5)
+    _, x2 = imp.generate(5)
+    assert not x1.any() and x2[0, 0, 2] == 1.0 and np.count_nonzero(x2) == 1
+
+
+def test_sgcht_testers_match_matlab_rules():
+    """TestPureTone.m: peak at frequency * nfft + 1 (1-based), else fail; every other bin
+    <= -60 dB re the peak.  TestImpulse.m: nothing above -60 dB (absolute) outside +-1 of
+    offset - current + 1; current advances by the block length."""
+    from ska_pst_dsp_model_amd import streaming as sgcht
+    t = np.arange(1024)
+    tone = np.exp(2j * np.pi * 0.25 * t)[None, None, :]
+    assert sgcht.TestPureTone(frequency=0.25).test(tone)[1] == 0
+    assert sgcht.TestPureTone(frequency=0.125).test(tone)[1] == -1          # wrong bin
+    spur = tone + 2e-3 * np.exp(2j * np.pi * 0.5 * t)[None, None, :]        # -54 dB
+    assert sgcht.TestPureTone(frequency=0.25).test(spur)[1] == -1
+    x = np.zeros((1, 1, 100), np.complex64)
+    x[0, 0, 40] = 1.0
+    x[0, 0, 41] = 0.5
+    ti = sgcht.TestImpulse(offset=40)   # 1-based off = 41: samples 40..42 (1-based) exempt
+    assert ti.test(x)[1] == 0 and ti.current == 100
+    x2 = np.zeros((1, 1, 100), np.complex64)
+    x2[0, 0, 45] = 2e-3                  # -54 dB, next block
+    assert sgcht.TestImpulse(offset=40).test(x2)[1] == -1
+
+
+def test_sgcht_without_channelizer_passes():
+    """sgcht(signal=..., test=true) with no cfg: the generators straight into the testers
+    (the first case of test_sgcht.m) — no device needed."""
+    from ska_pst_dsp_model_amd import streaming as sgcht
+    assert sgcht.sgcht(signal="complex_sinusoid", blocks=3, blocksz=4096).result == 0
+    r = sgcht.sgcht(signal="temporal_impulse", blocks=3, blocksz=16384)
+    assert r.result == 0 and r.tester.current == 3 * 16384

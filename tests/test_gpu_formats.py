@@ -253,6 +253,13 @@ def test_filterbank_strided_rejects(gpu):
         with pytest.raises(PfbError) as e:
             plan.execute_strided(x, out, 256 * 256, rs, cs, sel)
         assert e.value.status == PFB_ERR_INVALID_ARG and plan.buffered_samples == 0
+    # a stride whose furthest write lies beyond the buffer: rejected, nothing written
+    from ska_pst_dsp_model_amd._lib import PFB_ERR_BUFFER_TOO_SMALL
+    small_out = torch.zeros((1, 256, 100), dtype=torch.complex64, device=x.device)
+    with pytest.raises(PfbError) as e:
+        plan.execute_strided(x, small_out, 256 * 100, 1, 100)   # 208 rows into 100-sample runs
+    assert e.value.status == PFB_ERR_BUFFER_TOO_SMALL and plan.buffered_samples == 0
+    assert not small_out.abs().any()
 
 
 def test_two_stage_strided_matches_oracle(gpu):
