@@ -38,20 +38,49 @@ def summary(recs, seconds, world):
             "seconds": round(seconds, 1)}
 
 
+def stub_sweep(verify, npoints, rank, world, max_vectors=0):
+    """The sweep's vector list and round-robin share (verify.purity_sweep's, 'mid'
+    alignment), each vector 'scored' with fixed synthetic numbers that name its rank."""
+    al = verify.performance_alignment(4096, "8/7", 512, 128, 100353, 3, 0, 0)
+    items = verify.sweep_vectors(al, npoints, 3) + [("comb", 32), ("square_wave", 3981)]
+    if max_vectors:
+        items = items[:max_vectors]
+    recs = []
+    for kind, p in verify.shard(items, rank, world):
+        r = {"domain": kind, "param": p, "rank": rank}
+        if kind == "time":
+            r.update(peak_index=p, expected_index=p, max_outside_pm1_dB=-80.0, max_spurious_dB=-90.0)
+        elif kind == "freq":
+            r.update(max_spurious_dB=-70.0, total_spurious_dB=-65.0, max_diff_dB=-100.0)
+        elif kind == "comb":
+            r.update(comb_test=0)
+        else:
+            r.update(on_power=1.0, off_power=0.0)
+        recs.append(r)
+    return recs
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--npoints", type=int, default=300)
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--max-vectors", type=int, default=0)
     ap.add_argument("--out-dir", default=os.path.join(REPO, "gpurun_out", "purity"))
+    ap.add_argument("--stub", action="store_true",
+                    help="test hook: score nothing on a device; each rank emits one synthetic "
+                         "record per vector of its round-robin share (exercises the sharding "
+                         "and the rank-file merge on the CPU)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     from ska_pst_dsp_model_amd import verify
     t0 = time.perf_counter()
-    recs = verify.purity_sweep(device=local, npoints=args.npoints, batch=args.batch, rank=rank,
-                               world=world, max_vectors=args.max_vectors)
+    if args.stub:
+        recs = stub_sweep(verify, args.npoints, rank, world, args.max_vectors)
+    else:
+        recs = verify.purity_sweep(device=local, npoints=args.npoints, batch=args.batch, rank=rank,
+                                   world=world, max_vectors=args.max_vectors)
     if world == 1:
         for r in recs:
             print(json.dumps(r), flush=True)

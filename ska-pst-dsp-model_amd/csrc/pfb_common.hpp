@@ -315,8 +315,13 @@ inline int cu_count() {
 // sampled / combined inputs of the two-stage inversion (nch2 = N de/nu, times combine;
 // TwoStageInverseFilterBank.m:102-118)
 inline bool mixed_chan_supported(int N) {
-  return N == 14 || N == 28 || N == 56 || N == 112 || N == 216 || N == 224 || N == 432 ||
-         N == 448 || N == 864;
+  switch (N) {
+    case 14: case 28: case 56: case 112: case 192: case 216: case 224: case 384: case 432:
+    case 448: case 768: case 864: case 896: case 1536: case 1792: case 3072: case 3584:
+      return true;
+    default:
+      return false;
+  }
 }
 
 inline bool pow2_supported(int N) {

@@ -240,6 +240,13 @@ template <> struct FFTPlan<28> { using type = Radices<4, 7>; };
 template <> struct FFTPlan<56> { using type = Radices<8, 7>; };
 template <> struct FFTPlan<432> { using type = Radices<16, 27>; };
 template <> struct FFTPlan<864> { using type = Radices<16, 6, 9>; };
+// ... and those channel counts times the combine factor (2 .. 16)
+template <> struct FFTPlan<384> { using type = Radices<16, 24>; };
+template <> struct FFTPlan<768> { using type = Radices<16, 16, 3>; };
+template <> struct FFTPlan<1536> { using type = Radices<16, 16, 6>; };
+template <> struct FFTPlan<1792> { using type = Radices<16, 16, 7>; };
+template <> struct FFTPlan<3072> { using type = Radices<16, 16, 12>; };
+template <> struct FFTPlan<3584> { using type = Radices<16, 16, 14>; };
 
 // Default LDS accessors for a batch of rows stored at base + row * rs.
 struct LdsIO {

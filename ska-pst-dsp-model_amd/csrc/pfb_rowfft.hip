@@ -70,6 +70,14 @@ hipError_t dispatch_row_fft(int N, const RowFftArgs& r, int n_pol, hipStream_t s
       case 432: return launch_row_fft<432, DIR>(r, n_pol, s);
       case 448: return launch_row_fft<448, DIR>(r, n_pol, s);
       case 864: return launch_row_fft<864, DIR>(r, n_pol, s);
+      case 192: return launch_row_fft<192, DIR>(r, n_pol, s);
+      case 384: return launch_row_fft<384, DIR>(r, n_pol, s);
+      case 768: return launch_row_fft<768, DIR>(r, n_pol, s);
+      case 896: return launch_row_fft<896, DIR>(r, n_pol, s);
+      case 1536: return launch_row_fft<1536, DIR>(r, n_pol, s);
+      case 1792: return launch_row_fft<1792, DIR>(r, n_pol, s);
+      case 3072: return launch_row_fft<3072, DIR>(r, n_pol, s);
+      case 3584: return launch_row_fft<3584, DIR>(r, n_pol, s);
       default: break;
     }
   }

@@ -16,10 +16,11 @@
 //   pass 3   16-point IDFT over f1       -> y[t1a + RW t1b], stored when t1 is kept.
 // A wave holds 4 output phases in passes 1-2 (64 lanes), a 256-thread workgroup 16
 // adjacent phases (one 128-B line of every Z row and output row).
-// Memory access in whole lines: the stage-1 rows come in the blocked layout the streaming
-// analysis writes for this kernel (AnalysisArgs::zblk: 16 rows of one phase are one 128-B
-// run), so one load instruction reads rows 16 rb .. 16 rb + 15 of the wave's 4 phases as
-// 512 contiguous bytes; swap 2 is the one exchange that crosses waves: pass 3 lane (phase,
+// Memory access in wide segments: the stage-1 rows come in the run layout the streaming
+// analysis writes for this kernel (AnalysisArgs::zblk = ZB: ZB consecutive rows of one
+// phase are adjacent), so one load instruction reads ZB rows x the wave's 4 phases as one
+// contiguous 32 ZB-byte segment per row group (ZB = 2, the default: 8 segments of 64 B
+// instead of 16 of 32 B); swap 2 is the one exchange that crosses waves: pass 3 lane (phase,
 // t1a) of wave w takes t1a = w + 4 slot for all 16 phases, so one store instruction writes
 // 4 whole 128-B output rows.  Swap 1 stays inside the wave (LDS instructions of one wave
 // execute in order); two workgroup barriers per block order swap 2 (before its reads, and
@@ -140,8 +141,7 @@ void synth_wave_kernel(SynthBlockArgs a) {
 
   // stage-1 rows in runs of ZB rows per phase (AnalysisArgs::zblk): row ZB g + gi of phase
   // t at Z[(g N + t) ZB + gi]; ZB = 1 is the plain [row][t0] layout.  Row 16 r + l of the
-  // block: lane constant + r 16 N (the register's immediate).  ZB = 4 or 16: one load
-  // instruction reads whole 128-B lines
+  // block: lane constant + r 16 N (the register's immediate)
   const int ZB = max(a.zblk, 1);
   const float2* zpol = a.Z + pol * a.z_pol_stride + (int64_t)(t0g + wave * 4) * ZB;
   const uint32_t zbytes = (tmask(a.timing_mask) & 1) ? 0u : (uint32_t)((16 * 16 * N) * 8);

@@ -107,6 +107,8 @@ class TestPureTone:
             for ichan in range(nchan):
                 v = x[ipol, ichan, :].astype(np.complex128)
                 nfft = min(v.shape[0], max_nfft)
+                if nfft == 0:  # an empty block: Matlab's max([]) is empty and nothing fails
+                    continue
                 v = v[:nfft]
                 exp_index = self.frequency * nfft + 1
                 with np.errstate(divide="ignore"):
@@ -155,6 +157,9 @@ class TestImpulse:
                     w = float(amp_dB[outside].max())
                     worst = max(worst, w)
                     if w > self.dB_max:
+                        # (the position advances even on a failure: sgcht.m stops at the
+                        # first one, a caller scoring every block does not)
+                        self.current += nsample
                         self.last = {"fail": "outside", "dB": w, "off": off}
                         return self, -1
         self.current += nsample

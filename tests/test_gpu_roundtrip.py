@@ -417,3 +417,32 @@ def test_roundtrip_fused_and_chunked_paths_agree(gpu, case):
     assert torch.equal(chan_f, chan_c)
     assert_pfb_close(out_f.cpu().numpy(), out_c.cpu().numpy(), scale=1.0,
                      what="fused vs chunked round trip (raw)")
+
+
+def test_mid_external_matches_oracle(gpu):
+    """Reference sub-config 'mid_external' (config/test.config.json: SKA-Mid padded analysis,
+    4096 ch, 8/7, 100 353 taps, Nf 256, Ov 32 — so W = 224 at N = 4096, keep 192,
+    L_ov = 114 688) through the production round trip, 2^22 samples (1170 channelised
+    rows, 5 synthesis blocks), against orc.polyphase_analysis_padded ->
+    orc.polyphase_synthesis: channelised product at unit amplitude (RMS), output raw."""
+    import torch
+    pfb = _pfb()
+    cfg = pfb.default_config("mid_external")
+    assert (cfg.channels, cfg.input_fft_length, cfg.input_overlap) == (4096, 256, 32)
+    taps = _mid_taps(pfb)
+    n = 1 << 22
+    x = _np_noise(9, n)[None, None, :]
+    ana = pfb.AnalysisPlan(taps, 4096, "8/7", "polyphase_analysis_padded", 1, 0)
+    win = pfb.PFBWindow().lookup["tukey"](256, 32)
+    syn = pfb.SynthesisPlan(4096, "8/7", 256, 32, True, 1, True, taps, win, None, 1, 0)
+    chan, out = pfb.roundtrip(ana, syn, torch.from_numpy(x[:, 0, :]).to(gpu))
+    torch.cuda.synchronize()
+    ref_chan = orc.polyphase_analysis_padded(x, taps, 4096, "8/7")
+    assert ref_chan.shape == (1, 4096, 1170)
+    assert_pfb_close(chan.cpu().numpy().transpose(0, 2, 1), ref_chan, what="mid_external analysis")
+    ref = orc.polyphase_synthesis(ref_chan, 1, 256, "8/7",
+                                  {"apply_deripple": 1, "filter_coeff": taps}, 1, 32,
+                                  orc.pfb_window("tukey", 256, 32))
+    assert ref.shape == (1, 1, 5 * (917504 - 2 * 114688))
+    assert_pfb_close(out.cpu().numpy()[:, None, :], ref, scale=1.0,
+                     what="mid_external round trip (raw)")

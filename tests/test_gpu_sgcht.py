@@ -61,7 +61,13 @@ def _run_chain(pfb, signal, cfg_name, two_stage=False, invert=False, critical=Fa
         got = y.cpu().numpy() if hasattr(y, "cpu") else np.asarray(y)
         assert got.shape == ref.shape, f"block {i}: shape {got.shape} != {ref.shape}"
         if got.size:
-            assert_pfb_close(got, ref, scale=1.0 if invert else "rms",
+            # single-stage inverse: the unit-amplitude time series, raw (the reference's
+            # criterion); channelised data (fine channels, or the coarse channels an
+            # inverted second stage gives back, which carry stage 1's gain N |h|): at unit
+            # amplitude, by the peak for the two-stage bank — a tone's bins and the
+            # stopband leakage of 65 536 fine / 256 coarse channels span many decades
+            scale = 1.0 if (invert and not two_stage) else ("peak" if two_stage else "rms")
+            assert_pfb_close(got, ref, scale=scale,
                              what=f"sgcht {cfg_name} {signal} 2stg={two_stage} inv={invert} "
                                   f"crit={critical} comb={combine} block {i}")
             n_cmp += 1
@@ -70,16 +76,20 @@ def _run_chain(pfb, signal, cfg_name, two_stage=False, invert=False, critical=Fa
 
 
 CHAIN_CASES = [
-    # (cfg, signal, two_stage, invert, critical, combine, blocks, blocksz)
+    # (cfg, signal, two_stage, invert, critical, combine, blocks, blocksz): test_sgcht.m:5-51
+    # (single stage: 64 Ki-sample blocks as sgcht.m:484-485; two-stage: 2 blocks, long
+    # enough that the inverted second stage has whole synthesis blocks — sgcht.m uses 64 Mi)
     ("low", "complex_sinusoid", False, False, False, 1, 16, 1 << 16),
     ("low", "complex_sinusoid", False, True, False, 1, 16, 1 << 16),
     ("low", "temporal_impulse", False, True, False, 1, 16, 1 << 16),
     ("low_8_7", "complex_sinusoid", False, True, False, 1, 16, 1 << 16),
     ("low_8_7", "temporal_impulse", False, True, False, 1, 16, 1 << 16),
     ("low", "complex_sinusoid", True, False, False, 1, 2, 1 << 20),
-    ("low", "complex_sinusoid", True, True, False, 1, 2, 1 << 20),
+    ("low", "complex_sinusoid", True, True, False, 1, 2, 1 << 23),
     ("low", "complex_sinusoid", True, False, True, 1, 2, 1 << 20),
-    ("low", "complex_sinusoid", True, True, True, 1, 2, 1 << 20),
+    ("low", "complex_sinusoid", True, True, True, 1, 2, 1 << 23),
+    ("low", "complex_sinusoid", True, True, True, 16, 2, 1 << 23),
+    ("low_8_7", "temporal_impulse", True, True, True, 16, 2, 1 << 23),
 ]
 
 
@@ -89,17 +99,50 @@ def test_sgcht_chain_matches_oracle_chain(gpu, case):
     _run_chain(_pfb(), sig, cfg, two, inv, crit, comb, blocks, blocksz)
 
 
+def _tester_for(pfb, res, signal):
+    t = res.tester
+    return (pfb.TestPureTone(frequency=t.frequency) if signal == "complex_sinusoid"
+            else pfb.TestImpulse(offset=t.offset))
+
+
 @pytest.mark.parametrize("cfg", ["low", "low_8_7"])
 @pytest.mark.parametrize("signal", ["complex_sinusoid", "temporal_impulse"])
-def test_sgcht_invert_passes_reference_testers(gpu, cfg, signal):
-    """sgcht(signal, test=true, cfg, invert=true) returns 0: every streamed output block
-    has its tone at bin frequency * nfft + 1 with <= -60 dB elsewhere (TestPureTone.m), or
-    no sample above -60 dB outside +-1 of the delta's expected position (TestImpulse.m,
-    offset per sgcht.m:440-446)."""
+def test_sgcht_invert_reference_testers_agree_with_oracle_chain(gpu, cfg, signal):
+    """sgcht(signal, test=true, cfg, invert=true): every streamed output block scored by
+    TestPureTone.m (tone at bin frequency * nfft + 1, <= -60 dB elsewhere) or
+    TestImpulse.m (<= -60 dB outside +-1 of the delta, offset per sgcht.m:440-446).  The
+    device chain must give the oracle chain's verdict and worst level (within 0.5 dB
+    above -90 dB) on every block.  'low' passes every block.  'low_8_7' runs on taps from
+    the configuration's fir_design (the reference's Prototype_FIR.new.8-7 .npy file is
+    not in its repository): the impulse passes after the first output block (the
+    filters' start-up from zero state, -44 dB); the tone's spurious response is -55.4 dB
+    in every block in BOTH chains — a property of that designed filter at 8/7, which
+    sgcht.m would report as a failure — so only agreement is asserted there."""
     pfb = _pfb()
-    res = pfb.sgcht(signal=signal, cfg=cfg, invert=True, blocks=24, blocksz=1 << 16)
-    assert res.result == 0, res.tester.last
-    assert res.blocks == 24
+    res = pfb.sgcht(signal=signal, cfg=cfg, invert=True, blocks=24, blocksz=1 << 16,
+                    collect=True, test=False)
+    analysis, inverse = _oracle_chain(res.config, False, True, False, 1)
+    td, to = _tester_for(pfb, res, signal), _tester_for(pfb, res, signal)
+    def level(t):
+        d = t.last or {}
+        return next((d[k] for k in ("dB", "max_spurious_dB", "max_outside_dB") if k in d), None)
+
+    got, want, first = [], [], None
+    for i, (x, y) in enumerate(zip(res.inputs, res.outputs)):
+        ref = inverse.execute(analysis.execute(x))
+        got.append(td.test(y)[1])
+        want.append(to.test(ref)[1])
+        lg, lw = level(td), level(to)
+        if lw is not None and np.isfinite(lw) and lw > -90:
+            assert abs(lg - lw) < 0.5, f"block {i}: device {lg:.2f} dB vs oracle chain {lw:.2f} dB"
+        if first is None and ref.shape[-1]:
+            first = i
+    assert got == want, f"device verdicts {got} != oracle chain verdicts {want}"
+    assert first is not None
+    if cfg == "low":
+        assert all(r == 0 for r in got), got
+    elif signal == "temporal_impulse":
+        assert all(r == 0 for r in got[first + 1:]), f"steady-state block failed: {got}"
 
 
 def test_sgcht_impulse_lands_where_the_tester_expects(gpu):
