@@ -238,6 +238,11 @@ struct OutLayout {
   int32_t split, shift, nsel;
 };
 
+static pfb::AnalysisArgs analysis_args(const pfb_analysis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
+                                       float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
+                                       int64_t K_total, float2* z, int64_t z_ps, int64_t z_row0, int64_t pad,
+                                       const OutLayout* lay, int zblk);
+
 static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
                                float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
                                int64_t K_total, hipStream_t s, float2* z = nullptr,
@@ -261,6 +266,30 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
     HIPCHK(pfb::launch_lowcbf(l, s));
     return PFB_OK;
   }
+  pfb::AnalysisArgs a = analysis_args(p, in, in_ps, n_dat, out, out_ps, row0, K_end, K_total, z, z_ps, z_row0,
+                                      pad, lay, zblk);
+  a.scratch = nullptr;
+  if (!p->fused && !z) {
+    HIPCHK(p->scratch.ensure((size_t)p->n_pol * (K_end - row0) * p->N * sizeof(float2)));
+    a.scratch = p->scratch.as<float2>();
+  }
+  // algorithmic bytes: each input sample read once (the rows' new samples, the tail of
+  // the series with the last rows), each output sample written once
+  const int64_t in_samples = (K_end == K_total && row0 == 0)
+                                 ? n_dat
+                                 : (K_end - row0) * p->M + (K_end == K_total ? n_dat - K_total * p->M : 0);
+  // (with z: the stage-1 rows are a synthesis intermediate, not algorithmic bytes —
+  // the synthesis' algorithmic read of its input is counted by the block kernel)
+  const double bytes = (double)p->n_pol * (8.0 * in_samples + 8.0 * (K_end - row0) * p->N);
+  ProfScope ps(z ? 3 : 0, bytes, s, p->fused);  // generic path = FIR + row FFT launches
+  HIPCHK(pfb::launch_analysis(a, s));
+  return PFB_OK;
+}
+
+static pfb::AnalysisArgs analysis_args(const pfb_analysis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
+                                       float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
+                                       int64_t K_total, float2* z, int64_t z_ps, int64_t z_row0, int64_t pad,
+                                       const OutLayout* lay, int zblk) {
   pfb::AnalysisArgs a{};
   a.z = z;
   a.z_pol_stride = z_ps;
@@ -292,22 +321,7 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
     a.sel_shift = lay->shift;
     a.sel_n = lay->nsel;
   }
-  a.scratch = nullptr;
-  if (!p->fused && !z) {
-    HIPCHK(p->scratch.ensure((size_t)p->n_pol * (K_end - row0) * p->N * sizeof(float2)));
-    a.scratch = p->scratch.as<float2>();
-  }
-  // algorithmic bytes: each input sample read once (the rows' new samples, the tail of
-  // the series with the last rows), each output sample written once
-  const int64_t in_samples = (K_end == K_total && row0 == 0)
-                                 ? n_dat
-                                 : (K_end - row0) * p->M + (K_end == K_total ? n_dat - K_total * p->M : 0);
-  // (with z: the stage-1 rows are a synthesis intermediate, not algorithmic bytes —
-  // the synthesis' algorithmic read of its input is counted by the block kernel)
-  const double bytes = (double)p->n_pol * (8.0 * in_samples + 8.0 * (K_end - row0) * p->N);
-  ProfScope ps(z ? 3 : 0, bytes, s, p->fused);  // generic path = FIR + row FFT launches
-  HIPCHK(pfb::launch_analysis(a, s));
-  return PFB_OK;
+  return a;
 }
 
 // the plan's analysis runs on the streaming kernel, which takes a read offset (pad)
@@ -686,6 +700,11 @@ struct pfb_synthesis_plan {
   DevBuf taper, gainj, sbuf0, sbuf1;  // spectral taper (L), deripple gains (W), scratch
   DevBuf Z, carry, work, stage_in, stage_out;
   int64_t buffered = 0;
+  // one-launch round trip (pfb_roundtrip.hip): progress words, the block schedule of the
+  // last call shape ([9] segment starts, then the blocks), the host-visible timeout word
+  DevBuf rt_prog, rt_sched;
+  int64_t rt_key[5] = {-1, -1, -1, -1, -1};
+  unsigned* rt_err = nullptr;  // pinned, mapped
 };
 
 static void hann_sym(int L, std::vector<double>& h) {
@@ -1097,8 +1116,9 @@ pfb_status pfb_synthesis_plan_destroy(pfb_synthesis_plan* p) {
   (void)hipSetDevice(p->device);
   for (DevBuf* b : {&p->window, &p->tw4, &p->tw4s, &p->twN, &p->twNf, &p->twW, &p->perm, &p->cgain,
                     &p->taper, &p->gainj, &p->sbuf0, &p->sbuf1, &p->Z, &p->carry, &p->work,
-                    &p->stage_in, &p->stage_out})
+                    &p->stage_in, &p->stage_out, &p->rt_prog, &p->rt_sched})
     b->release();
+  if (p->rt_err) (void)hipHostFree(p->rt_err);
   delete p;
   return PFB_OK;
 }
@@ -1285,6 +1305,162 @@ pfb_status pfb_inverse_filterbank_reset(pfb_synthesis_plan* p) {
 // `chan`.  On this chunked path every row and block is computed by the same kernels with
 // the same inputs as pfb_analysis_execute + pfb_synthesis_execute, so both results are
 // bit-identical to the separate calls (the fused path below: see its comment).
+// ------------------------------------------------------------- one-launch round trip
+#ifdef PFB_EXPERIMENTS
+// Synthesis block schedule of the fused kernel (pfb_roundtrip.hip): the analysis runs nA
+// contiguous step ranges (16 rows per step) side by side, ranges [x nA/8, (x+1) nA/8) on XCD
+// x; block b (rows z_row0 + b keep .. + Nf) belongs to the segment of its first range and is
+// ready once every range holding its rows has reached them — at the fraction of the range
+// below.  Each segment's blocks go to that XCD's synthesis workgroups in that order.
+static void round_trip_schedule(int64_t n_steps, int nA, int64_t z_row0, int keep, int Nf, int64_t B,
+                                std::vector<int>& sched) {
+  auto st0 = [&](int64_t w) { return n_steps * w / nA; };
+  auto range_of = [&](int64_t st) { return ((st + 1) * nA + n_steps - 1) / n_steps - 1; };
+  std::vector<std::vector<std::pair<double, int>>> segs(8);
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t r0 = z_row0 + b * keep;
+    const int64_t s_lo = r0 / 16, s_hi = std::min((r0 + Nf - 1) / 16, n_steps - 1);
+    double ready = 0.0;
+    for (int64_t w = range_of(s_lo); w <= range_of(s_hi); ++w) {
+      const int64_t a0 = st0(w), a1 = st0(w + 1);
+      ready = std::max(ready, (double)(std::min(s_hi + 1, a1) - a0) / (double)std::max<int64_t>(a1 - a0, 1));
+    }
+    const int x = (int)std::min<int64_t>(7, range_of(s_lo) / (nA / 8));
+    segs[(size_t)x].push_back({ready, (int)b});
+  }
+  sched.assign(9, 0);
+  for (int x = 0; x < 8; ++x) {
+    std::sort(segs[(size_t)x].begin(), segs[(size_t)x].end());
+    sched[(size_t)x + 1] = sched[(size_t)x] + (int)segs[(size_t)x].size();
+  }
+  for (int x = 0; x < 8; ++x)
+    for (const auto& e : segs[(size_t)x]) sched.push_back(e.second);
+}
+
+// The fused path as one launch when the shape, the residency (3 workgroups per CU) and
+// the polarisation count allow; *done = false leaves the call to the two-kernel path.
+static pfb_status roundtrip_one_launch(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, const float2* x,
+                                       int64_t in_ps, int64_t n_dat, float2* y, int64_t chan_ps, int64_t K,
+                                       int64_t off, int64_t B, float2* out, int64_t out_ps, int64_t olen,
+                                       hipStream_t s, bool* done) {
+  *done = false;
+  // measured and rejected: experiments build only, PFB_RT_ONE_LAUNCH=1
+  static const bool on = pfb::knob("PFB_RT_ONE_LAUNCH") && std::atoi(pfb::knob("PFB_RT_ONE_LAUNCH")) == 1;
+  if (!on) return PFB_OK;
+  const int cus = pfb::roundtrip_cu_count();
+  const int n_pol = pa->n_pol;
+  if (n_pol != 1 && n_pol != 2 && n_pol != 4) return PFB_OK;
+  const int nA = cus / n_pol, nS = 2 * cus / n_pol;
+  const int groups = ps->N / 16;
+  if (nA <= 0 || nA % 8 != 0 || nS % (8 * groups) != 0) return PFB_OK;
+  const int64_t zrows = (K - off + 15) / 16 * 16;
+  float2* Z = ps->Z.as<float2>();
+  const pfb::AnalysisArgs aa = analysis_args(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, Z, zrows * pa->N, off, 0,
+                                             nullptr, 2);
+  const pfb::SynthBlockArgs sa = synth_args(ps, Z, zrows * pa->N, 0, B, out, out_ps, olen, 2);
+  int per_cu = 0;
+  if (!pfb::roundtrip_fused_supported(aa, sa, &per_cu) || per_cu < 3) return PFB_OK;
+  // analysis steps of the call (launch_stream's count with row0 = 0)
+  const int64_t n_steps = ((K + pa->nu - 1) / pa->nu + (16 / pa->nu) - 1) / (16 / pa->nu);
+  if (n_steps < nA) return PFB_OK;  // every range at least one step
+  // a workgroup's rows must fit one buffer descriptor (launch_stream's rule)
+  if ((n_steps / nA + 2) * 16 * (int64_t)pa->N * 8 + 64 * (int64_t)pa->N * 8 > pfb::kRsrcMaxBytes) return PFB_OK;
+  const int64_t key[5] = {n_steps, nA, off, B, ps->keep};
+  if (!std::equal(key, key + 5, ps->rt_key)) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(s, &cs));
+    if (cs != hipStreamCaptureStatusNone) return PFB_OK;  // schedule upload is synchronous
+    std::vector<int> sched;
+    round_trip_schedule(n_steps, nA, off, ps->keep, ps->Nf, B, sched);
+    HIPCHK(upload(ps->rt_sched, sched));
+    HIPCHK(ps->rt_prog.ensure((size_t)n_pol * nA * pfb::kProgStride * 4));
+    if (!ps->rt_err) {
+      HIPCHK(hipHostMalloc((void**)&ps->rt_err, 16, hipHostMallocMapped | hipHostMallocCoherent));
+      *ps->rt_err = 0;
+    }
+    std::copy(key, key + 5, ps->rt_key);
+  }
+  if (__atomic_load_n(ps->rt_err, __ATOMIC_ACQUIRE) != 0) {
+    *ps->rt_err = 0;
+    return fail(PFB_ERR_HIP, "an earlier one-launch round trip gave up waiting for its stage-1 rows "
+                             "(workgroups not co-resident): its output is invalid");
+  }
+  unsigned* err_dev = nullptr;
+  HIPCHK(hipHostGetDevicePointer((void**)&err_dev, ps->rt_err, 0));
+  pfb::RtFusedArgs f{};
+  f.prog = ps->rt_prog.as<unsigned>();
+  f.err = err_dev;
+  f.seg = ps->rt_sched.as<int>();
+  f.order = f.seg + 9;
+  f.nA = nA;
+  f.nS = nS;
+  f.lanes = nS / (8 * groups);
+  f.n_steps = n_steps;
+  f.z_row0 = off;
+  static const int nowait = pfb::knob("PFB_RT_NOWAIT") ? std::atoi(pfb::knob("PFB_RT_NOWAIT")) : 0;
+  f.nowait = nowait;
+  static const int prio = pfb::knob("PFB_RT_PRIO") ? std::atoi(pfb::knob("PFB_RT_PRIO")) : 1;
+  f.prio = prio;
+  f.spin_max = 1u << 20;  // >= ~0.1 s per wait: far beyond any real wait
+  HIPCHK(hipMemsetAsync(ps->rt_prog.p, 0, ps->rt_prog.bytes, s));
+  {
+    // algorithmic bytes of the whole round trip (input + channelised product written and
+    // read + output), profiled as one launch
+    const double bytes = (double)n_pol * (8.0 * n_dat + 16.0 * K * pa->N + 8.0 * olen);
+    ProfScope pr(3, bytes, s);
+    HIPCHK(pfb::launch_roundtrip_fused(aa, sa, f, s));
+  }
+  *done = true;
+  return PFB_OK;
+}
+#endif  // PFB_EXPERIMENTS
+
+constexpr bool kPolStreamsDefault = false;  // (A/B: PFB_RT_POL_STREAMS)
+
+// Two or more polarisations (independent series): polarisation p's round trip runs on
+// stream p % 2 (the caller's stream and the plan's aux stream) and its analysis starts
+// after polarisation p-1's analysis, so it runs beside p-1's synthesis — the HBM-bound
+// analysis and the latency-bound synthesis overlap instead of taking turns.  Each launch
+// is the single-polarisation form of the fused path (bit-identical per polarisation).
+static pfb_status roundtrip_pol_streams(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, const float2* x,
+                                        int64_t in_ps, int64_t n_dat, float2* y, int64_t chan_ps, int64_t K,
+                                        int64_t off, int64_t z0, int64_t B, float2* Z, int64_t zrows, int zblk,
+                                        float2* out, int64_t out_ps, int64_t olen, hipStream_t s) {
+  const int n_pol = pa->n_pol;
+  if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));
+  while ((int64_t)pa->events.size() < n_pol + 2) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    pa->events.push_back(e);
+  }
+  hipStream_t st[2] = {s, pa->aux};
+  HIPCHK(hipEventRecord(pa->events[0], s));
+  HIPCHK(hipStreamWaitEvent(pa->aux, pa->events[0], 0));
+  const int64_t zps = zrows * pa->N;
+  for (int p = 0; p < n_pol; ++p) {
+    hipStream_t q = st[p & 1];
+    if (p > 0) HIPCHK(hipStreamWaitEvent(q, pa->events[(size_t)p], 0));  // after p-1's analysis
+    pfb::AnalysisArgs a = analysis_args(pa, x + p * in_ps, in_ps, n_dat, y + p * chan_ps, chan_ps, 0, K, K,
+                                        Z + p * zps, zps, z0, 0, nullptr, zblk);
+    a.n_pol = 1;
+    {
+      ProfScope pr(3, 8.0 * n_dat + 8.0 * K * pa->N, q, pa->fused);
+      HIPCHK(pfb::launch_analysis(a, q));
+    }
+    HIPCHK(hipEventRecord(pa->events[(size_t)p + 1], q));
+    pfb::SynthBlockArgs b = synth_args(ps, Z + p * zps + (off - z0) * pa->N, zps, 0, B, out + p * out_ps, out_ps,
+                                       olen, zblk);
+    b.n_pol = 1;
+    {
+      ProfScope pr(2, (double)B * ps->keep * ps->N * 8.0 + (double)B * ps->Lkeep * 8.0, q);
+      HIPCHK(pfb::launch_synth_block(b, q));
+    }
+  }
+  HIPCHK(hipEventRecord(pa->events[(size_t)n_pol + 1], pa->aux));
+  HIPCHK(hipStreamWaitEvent(s, pa->events[(size_t)n_pol + 1], 0));
+  return PFB_OK;
+}
+
 pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, const pfb_cf32* in,
                                  int64_t in_ps, int64_t n_dat, pfb_cf32* chan, int64_t chan_ps,
                                  int64_t chan_cap, int64_t* n_chan_rows, int64_t sample_offset,
@@ -1355,13 +1531,58 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
       return fail(PFB_ERR_HIP, "round trip stage-1 rows (%zu bytes): %s", zbytes, hipGetErrorString(ze));
     }
   }
+#ifdef PFB_EXPERIMENTS
+  if (fuse && zblk == 2) {
+    bool done = false;
+    pfb_status st = roundtrip_one_launch(pa, ps, x, in_ps, n_dat, y, chan_ps, K, off, B, (float2*)out, out_ps,
+                                         olen, s, &done);
+    if (st != PFB_OK || done) return st;
+  }
+#endif
   if (fuse) {
     float2* Z = ps->Z.as<float2>();
-    pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0,
-                                 nullptr, zblk);
-    if (st != PFB_OK) return st;
-    return synthesis_blocks(ps, Z + (off - z0) * pa->N, zrows * pa->N, 0, B, (float2*)out, out_ps,
-                            olen, s, zblk);
+    static const int conc = pfb::knob("PFB_RT_CONC") ? std::atoi(pfb::knob("PFB_RT_CONC")) : 1;
+    const int64_t C = std::min<int64_t>(std::max(conc, 1), B);
+    static const bool pol_streams = kPolStreamsDefault ? !(pfb::knob("PFB_RT_POL_STREAMS") && std::atoi(pfb::knob("PFB_RT_POL_STREAMS")) == 0)
+                                                       : (pfb::knob("PFB_RT_POL_STREAMS") && std::atoi(pfb::knob("PFB_RT_POL_STREAMS")) == 1);
+    if (pa->n_pol >= 2 && pol_streams && C <= 1)
+      return roundtrip_pol_streams(pa, ps, x, in_ps, n_dat, y, chan_ps, K, off, z0, B, Z, zrows, zblk,
+                                   (float2*)out, out_ps, olen, s);
+    if (C <= 1 || !zblk) {
+      pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0,
+                                   nullptr, zblk);
+      if (st != PFB_OK) return st;
+      return synthesis_blocks(ps, Z + (off - z0) * pa->N, zrows * pa->N, 0, B, (float2*)out, out_ps,
+                              olen, s, zblk);
+    }
+    // (experiments) C chunks of blocks: the analysis of chunk c+1 on the aux stream runs
+    // beside the synthesis of chunk c (rows in whole 16-row steps from `off`)
+    if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));
+    while ((int64_t)pa->events.size() < C + 2) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      pa->events.push_back(e);
+    }
+    HIPCHK(hipEventRecord(pa->events[0], s));
+    HIPCHK(hipStreamWaitEvent(pa->aux, pa->events[0], 0));
+    int64_t ra = 0;
+    for (int64_t c = 0; c < C; ++c) {
+      const int64_t b_lo = B * c / C, b_hi = B * (c + 1) / C;
+      int64_t rb = (c == C - 1) ? K : off + ((b_hi * ps->keep + 2 * (int64_t)ps->Ov + 15) / 16) * 16;
+      rb = std::max(ra, std::min(K, rb));
+      pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, ra, rb, K, pa->aux, Z, zrows * pa->N,
+                                   z0, 0, nullptr, zblk);
+      if (st != PFB_OK) return st;
+      ra = rb;
+      HIPCHK(hipEventRecord(pa->events[1 + c], pa->aux));
+      HIPCHK(hipStreamWaitEvent(s, pa->events[1 + c], 0));
+      st = synthesis_blocks(ps, Z + (off - z0 + b_lo * ps->keep) * pa->N, zrows * pa->N, b_lo, b_hi - b_lo,
+                            (float2*)out, out_ps, olen, s, zblk);
+      if (st != PFB_OK) return st;
+    }
+    HIPCHK(hipEventRecord(pa->events[1 + C], pa->aux));
+    HIPCHK(hipStreamWaitEvent(s, pa->events[1 + C], 0));
+    return PFB_OK;
   }
 
   if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));

@@ -27,216 +27,9 @@
 // before the next block's swap 1 rewrites the tiles other waves read).  Every twiddle is a
 // table entry rounded once from double; the per-lane gain x twiddle values (t4, 14 complex)
 // are constant for the workgroup's whole block range and loaded once per launch.
-#include "pfb_common.hpp"
+#include "pfb_synth_wave.hpp"
 
 namespace pfb {
-
-namespace {
-
-constexpr int kWgThreads = 256;
-constexpr int kCols = 16;        // output phases per workgroup
-// LDS: one 16 x 16 tile per phase, rows of 144 B (16 values + 16 B), the tile of phase
-// col = 4 w + cc at col * 2560 + 16 (w + 4 cc) bytes.  With lane = 4 l + cc in passes 1-2
-// and lane = 16 slot + col in pass 3, every ds_read_b128 of either swap is conflict-free
-// (the 16-lane groups of MI355X_MICROARCH.md §LDS land on 16 different 16-B bank units),
-// the ds_write_b64 of the swaps are at most 2-way, and every address is a lane constant
-// plus an immediate.
-constexpr int kRowB = 144;
-constexpr int kColStride = 2560;
-constexpr int kTilesB = kCols * kColStride;
-constexpr int kTw2RowB = 112;    // tw2 row: 14 values (RW <= 14)
-constexpr int kWinRowB = 80;     // window row: 16 floats + 16 B pad
-constexpr int kTw1Off = kTilesB;
-constexpr int kTw2Off = kTw1Off + 16 * kRowB;
-constexpr int kWinOff = kTw2Off + 16 * kTw2RowB;
-constexpr int kLdsB = kWinOff + 16 * kWinRowB;
-
-__device__ __forceinline__ int col_base(int col) { return col * kColStride + 16 * ((col >> 2) + 4 * (col & 3)); }
-
-// 2 consecutive float2 of an LDS row (one ds_read_b128)
-__device__ __forceinline__ void lds_pair(const char* p, float2& a, float2& b) {
-  const v4f q = *reinterpret_cast<const v4f*>(p);
-  a = make_float2(q.x, q.y);
-  b = make_float2(q.z, q.w);
-}
-
-// kept slot r'' of pass-2 bin f2 (f = f1 + 16 f2), -1 if discarded; H = RW / 2
-template <int RW, bool SPANS>
-constexpr int kept_r(int f2) {
-  constexpr int H = RW / 2;
-  if (f2 < H) return SPANS ? f2 : f2 + H;
-  if (f2 >= 16 - H) return SPANS ? f2 - (16 - RW) : f2 - (16 - H);
-  return -1;
-}
-// pass-2 bin of kept slot r''
-template <int RW, bool SPANS>
-constexpr int bin_of(int rr) {
-  for (int f2 = 0; f2 < 16; ++f2)
-    if (kept_r<RW, SPANS>(f2) == rr) return f2;
-  return -1;
-}
-
-}  // namespace
-
-// DK: overlap reuse, keep = 16 DK (the next block's rows l + 16 r, r < 16 - DK, are this
-// block's registers r + DK).
-template <int RW, bool SPANS, int DK>
-__global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(3)))
-void synth_wave_kernel(SynthBlockArgs a) {
-  constexpr int W = 16 * RW;
-  static_assert(RW <= 14 && RW % 2 == 0, "W = 16 RW with RW even and <= 14");
-  static_assert(DK >= 1 && DK <= 16, "keep = 16 DK");
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int l = lane >> 2;         // FFT lane within the phase (passes 1-2)
-  const int cc = lane & 3;         // phase within the wave (passes 1-2)
-  const int col = wave * 4 + cc;   // phase within the workgroup (passes 1-2)
-  const int N = a.N;
-  const int groups = N / kCols;
-  const int lt = xcd_tile(blockIdx.x, gridDim.x);
-  const int tg = lt % groups;
-  const int rr = lt / groups;
-  const int Rg = gridDim.x / groups;
-  const int b_begin = (int)((int64_t)a.n_blocks * rr / Rg);
-  const int b_end = (int)((int64_t)a.n_blocks * (rr + 1) / Rg);
-  if (b_begin >= b_end) return;  // uniform per workgroup: no barrier is skipped by part of it
-  const int t0g = tg * kCols;    // the workgroup's first output phase
-  const int pol = blockIdx.y;
-
-  // ---- tables (once per launch): tw1[i][f1] = e^{-2 pi i i f1 / 256}, tw2[f1][t1a] =
-  // e^{+2 pi i f1 t1a / W}, window transposed winT[i][r] = win[i + 16 r]
-  for (int e = tid; e < 256; e += kWgThreads) {
-    const int i = e >> 4, f = e & 15;
-    *reinterpret_cast<float2*>(lds + kTw1Off + i * kRowB + f * 8) = a.twNf[(i * f) & 255];
-    if (f < RW) {
-      float2 w = a.twW[(i * f) % W];  // e^{-2 pi i m / W}: conjugate for the inverse
-      w.y = -w.y;
-      *reinterpret_cast<float2*>(lds + kTw2Off + i * kTw2RowB + f * 8) = w;
-    }
-    *reinterpret_cast<float*>(lds + kWinOff + i * kWinRowB + f * 4) = a.window[i + 16 * f];
-  }
-  // ---- lane constants: gain x four-step twiddle x output scale of the kept bins
-  // j' = l + 16 r'' at phase t0g + col (table [j'][t0], scale folded on the host)
-  float2 t4[RW];
-  {
-    const __amdgpu_buffer_rsrc_t tr = make_rsrc(a.tw4s + t0g, (uint32_t)((W - 1) * N + kCols) * 8u);
-    static_for<0, RW>([&](auto r) {
-      const v2u x = __builtin_amdgcn_raw_buffer_load_b64(tr, (uint32_t)(((l + 16 * r) * N + col) * 8), 0, 0);
-      t4[r] = __builtin_bit_cast(float2, x);
-    });
-  }
-  __syncthreads();  // tables staged
-
-  // swap addresses (lane constants; the row / register offsets are immediates)
-  const int wr = col_base(col) + 8 * l;               // swap writes: slot l of rows 0..15
-  const int rd1 = col_base(col) + l * kRowB;          // swap 1 reads: row l
-  const int col2 = lane & 15;                         // pass 3: phase
-  const int t1a = wave + 4 * (lane >> 4);             // pass 3: t1a (valid below RW)
-  const int rd2 = col_base(col2) + min(t1a, 15) * kRowB;
-  const char* tw1row = lds + kTw1Off + l * kRowB;
-  const char* tw2row = lds + kTw2Off + l * kTw2RowB;
-  const char* winrow = lds + kWinOff + l * kWinRowB;
-
-  // stage-1 rows in runs of ZB rows per phase (AnalysisArgs::zblk): row ZB g + gi of phase
-  // t at Z[(g N + t) ZB + gi]; ZB = 1 is the plain [row][t0] layout.  Row 16 r + l of the
-  // block: lane constant + r 16 N (the register's immediate)
-  const int ZB = max(a.zblk, 1);
-  const float2* zpol = a.Z + pol * a.z_pol_stride + (int64_t)(t0g + wave * 4) * ZB;
-  const uint32_t zbytes = (tmask(a.timing_mask) & 1) ? 0u : (uint32_t)((16 * 16 * N) * 8);
-  const uint32_t zlane = (uint32_t)((((l / ZB) * N) * ZB + cc * ZB + l % ZB) * 8);
-  float2* opol = a.out + pol * a.out_pol_stride;
-
-  float2 x[16];  // raw Z values of the next block, rows l + 16 r
-  auto prefetch = [&](int b, auto reuse) {
-    constexpr int R0 = decltype(reuse)::value ? 16 - DK : 0;
-    static_for<0, R0>([&](auto r) { x[r] = x[r + DK]; });
-    const __amdgpu_buffer_rsrc_t z = make_rsrc(zpol + (int64_t)b * a.keep * N, zbytes);
-    static_for<R0, 16>([&](auto r) {
-      const v2u v = __builtin_amdgcn_raw_buffer_load_b64(z, zlane, r * N * 16 * 8, 0);
-      x[r] = __builtin_bit_cast(float2, v);
-    });
-  };
-  prefetch(b_begin, std::false_type{});
-
-#pragma unroll 1
-  for (int b = b_begin; b < b_end; ++b) {
-    // every wave has read the previous block's swap-2 data (from all tiles), and the
-    // four waves move through the Z and output lines together
-    __syncthreads();
-    // ---- pass 1: taper, 16-point DFT over r, twiddle
-    float2 v[16];
-    {
-      float wv[16];
-      static_for<0, 4>([&](auto k) {
-        const v4f q = *reinterpret_cast<const v4f*>(winrow + 16 * k);
-        wv[4 * k] = q.x;
-        wv[4 * k + 1] = q.y;
-        wv[4 * k + 2] = q.z;
-        wv[4 * k + 3] = q.w;
-      });
-      static_for<0, 16>([&](auto r) { v[r] = cscale(x[r], wv[r]); });
-    }
-    // the next block's rows (the last block re-reads itself: the wait count stays fixed)
-    prefetch(min(b + 1, b_end - 1), std::integral_constant<bool, (DK < 16)>{});
-    sdft<16, -1>(v);
-    {
-      float2 w[16];
-      static_for<0, 8>([&](auto k) { lds_pair(tw1row + 16 * k, w[2 * k], w[2 * k + 1]); });
-      static_for<1, 16>([&](auto f) { v[f] = cmul(v[f], w[f]); });
-    }
-    // ---- swap 1 (inside the wave): element (row f1, slot l) of this phase's tile
-    static_for<0, 16>([&](auto f) {
-      constexpr int fr = decltype(f)::value;
-      *reinterpret_cast<float2*>(lds + wr + fr * kRowB) = v[fr];
-    });
-    __builtin_amdgcn_wave_barrier();
-    static_for<0, 8>([&](auto k) {
-      lds_pair(lds + rd1 + 16 * k, v[2 * k], v[2 * k + 1]);
-    });
-    // ---- pass 2: 16-point DFT over i; kept bins x t4; RW-point IDFT; W-pass twiddle
-    sdft<16, -1>(v);
-    float2 u[RW];
-    static_for<0, RW>([&](auto r) {
-      constexpr int f2 = bin_of<RW, SPANS>(decltype(r)::value);
-      u[r] = cmul(v[f2], t4[r]);
-    });
-    sdft<RW, +1>(u);
-    {
-      float2 w[RW];
-      static_for<0, RW / 2>([&](auto k) { lds_pair(tw2row + 16 * k, w[2 * k], w[2 * k + 1]); });
-      static_for<1, RW>([&](auto t) { u[t] = cmul(u[t], w[t]); });
-    }
-    // ---- swap 2 (across the workgroup): element (row t1a, slot f1 = l) of this phase's
-    // tile (the wave's own swap-1 reads of the tile are issued before these writes)
-    __builtin_amdgcn_wave_barrier();
-    static_for<0, RW>([&](auto t) {
-      constexpr int tr = decltype(t)::value;
-      *reinterpret_cast<float2*>(lds + wr + tr * kRowB) = u[tr];
-    });
-    __syncthreads();
-    static_for<0, 8>([&](auto k) {
-      lds_pair(lds + rd2 + 16 * k, v[2 * k], v[2 * k + 1]);
-    });
-    // ---- pass 3: 16-point IDFT over f1 -> t1 = t1a + RW t1b; overlap-discard on the store
-    sdft<16, +1>(v);
-    {
-      const int64_t ob = (a.block0 + b) * (int64_t)a.Lkeep;  // first kept output sample
-      const int64_t avail = a.out_limit - ob;
-      const int64_t nk = (tmask(a.timing_mask) & 2)
-                             ? 0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
-      const __amdgpu_buffer_rsrc_t o = make_rsrc(opol + ob, (uint32_t)nk * 8u);
-      // lanes t1a >= RW hold no output: their offsets leave the descriptor's range (as do
-      // the discarded t1 < t1_lo, whose negative offsets wrap past 2^31)
-      const int base = (t1a < RW) ? ((t1a - a.t1_lo) * N + t0g + col2) * 8 : (int)0x80000000;
-      static_for<0, 16>([&](auto t) {
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v[t]), o,
-                                              (uint32_t)(base + t * RW * N * 8), 0, 0);
-      });
-    }
-  }
-}
 
 bool synth_wave_supported(const SynthBlockArgs& a) {
   if (a.Nf != 256 || (a.W != 224 && a.W != 192)) return false;
@@ -251,7 +44,9 @@ static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
   if (e != hipSuccess) return e;
   const int groups = a.N / kCols;
   // resident workgroups: 3 per CU (3 waves per SIMD at <= 168 VGPRs; LDS would allow 4)
-  const int per_cu = std::max(1, std::min(3, (160 * 1024) / kLdsB));
+  int per_cu = std::max(1, std::min(3, (160 * 1024) / kLdsB));
+  static const int env_wpc = knob("PFB_WAVE_PER_CU") ? std::atoi(knob("PFB_WAVE_PER_CU")) : 0;  // A/B
+  if (env_wpc > 0) per_cu = env_wpc;
   int ranges = std::max(1, cu_count() * per_cu / (groups * a.n_pol));
   ranges = std::min(ranges, a.n_blocks);
   dim3 grid((unsigned)(groups * ranges), (unsigned)a.n_pol);
