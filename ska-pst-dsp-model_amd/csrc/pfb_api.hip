@@ -1415,52 +1415,6 @@ static pfb_status roundtrip_one_launch(pfb_analysis_plan* pa, pfb_synthesis_plan
 }
 #endif  // PFB_EXPERIMENTS
 
-constexpr bool kPolStreamsDefault = false;  // (A/B: PFB_RT_POL_STREAMS)
-
-// Two or more polarisations (independent series): polarisation p's round trip runs on
-// stream p % 2 (the caller's stream and the plan's aux stream) and its analysis starts
-// after polarisation p-1's analysis, so it runs beside p-1's synthesis — the HBM-bound
-// analysis and the latency-bound synthesis overlap instead of taking turns.  Each launch
-// is the single-polarisation form of the fused path (bit-identical per polarisation).
-static pfb_status roundtrip_pol_streams(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, const float2* x,
-                                        int64_t in_ps, int64_t n_dat, float2* y, int64_t chan_ps, int64_t K,
-                                        int64_t off, int64_t z0, int64_t B, float2* Z, int64_t zrows, int zblk,
-                                        float2* out, int64_t out_ps, int64_t olen, hipStream_t s) {
-  const int n_pol = pa->n_pol;
-  if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));
-  while ((int64_t)pa->events.size() < n_pol + 2) {
-    hipEvent_t e;
-    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    pa->events.push_back(e);
-  }
-  hipStream_t st[2] = {s, pa->aux};
-  HIPCHK(hipEventRecord(pa->events[0], s));
-  HIPCHK(hipStreamWaitEvent(pa->aux, pa->events[0], 0));
-  const int64_t zps = zrows * pa->N;
-  for (int p = 0; p < n_pol; ++p) {
-    hipStream_t q = st[p & 1];
-    if (p > 0) HIPCHK(hipStreamWaitEvent(q, pa->events[(size_t)p], 0));  // after p-1's analysis
-    pfb::AnalysisArgs a = analysis_args(pa, x + p * in_ps, in_ps, n_dat, y + p * chan_ps, chan_ps, 0, K, K,
-                                        Z + p * zps, zps, z0, 0, nullptr, zblk);
-    a.n_pol = 1;
-    {
-      ProfScope pr(3, 8.0 * n_dat + 8.0 * K * pa->N, q, pa->fused);
-      HIPCHK(pfb::launch_analysis(a, q));
-    }
-    HIPCHK(hipEventRecord(pa->events[(size_t)p + 1], q));
-    pfb::SynthBlockArgs b = synth_args(ps, Z + p * zps + (off - z0) * pa->N, zps, 0, B, out + p * out_ps, out_ps,
-                                       olen, zblk);
-    b.n_pol = 1;
-    {
-      ProfScope pr(2, (double)B * ps->keep * ps->N * 8.0 + (double)B * ps->Lkeep * 8.0, q);
-      HIPCHK(pfb::launch_synth_block(b, q));
-    }
-  }
-  HIPCHK(hipEventRecord(pa->events[(size_t)n_pol + 1], pa->aux));
-  HIPCHK(hipStreamWaitEvent(s, pa->events[(size_t)n_pol + 1], 0));
-  return PFB_OK;
-}
-
 pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, const pfb_cf32* in,
                                  int64_t in_ps, int64_t n_dat, pfb_cf32* chan, int64_t chan_ps,
                                  int64_t chan_cap, int64_t* n_chan_rows, int64_t sample_offset,
@@ -1543,11 +1497,6 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
     float2* Z = ps->Z.as<float2>();
     static const int conc = pfb::knob("PFB_RT_CONC") ? std::atoi(pfb::knob("PFB_RT_CONC")) : 1;
     const int64_t C = std::min<int64_t>(std::max(conc, 1), B);
-    static const bool pol_streams = kPolStreamsDefault ? !(pfb::knob("PFB_RT_POL_STREAMS") && std::atoi(pfb::knob("PFB_RT_POL_STREAMS")) == 0)
-                                                       : (pfb::knob("PFB_RT_POL_STREAMS") && std::atoi(pfb::knob("PFB_RT_POL_STREAMS")) == 1);
-    if (pa->n_pol >= 2 && pol_streams && C <= 1)
-      return roundtrip_pol_streams(pa, ps, x, in_ps, n_dat, y, chan_ps, K, off, z0, B, Z, zrows, zblk,
-                                   (float2*)out, out_ps, olen, s);
     if (C <= 1 || !zblk) {
       pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0,
                                    nullptr, zblk);
