@@ -66,6 +66,10 @@ def parse():
                          "runs the synthesis channel IFFT on the rows it produces; the "
                          "channelised product is still written in full); 0: separate "
                          "analysis and synthesis calls")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="steps in flight: D plan pairs (each with its own stage-1-row, "
+                         "channelised and output buffers) on D streams, step i on pair i mod D, "
+                         "so one step's analysis can run beside the previous step's synthesis")
     ap.add_argument("--kernel-events", type=int, default=1,
                     help="record HIP events around every kernel in the timed region")
     ap.add_argument("--e2e", type=int, default=0,
@@ -435,47 +439,71 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
     x = torch.stack(xs).to(torch.complex64).contiguous()
     del xs
 
-    ana = pfb.AnalysisPlan(taps, N_CHAN, OS_STR, "polyphase_analysis", n_pol, local)
     win = pfb.PFBWindow().lookup["tukey"](NF, OV)
-    syn = pfb.SynthesisPlan(N_CHAN, OS_STR, NF, OV, True, 1, True, taps, win, None, n_pol, local)
-    if args.chunk_blocks:
-        syn.set_chunk_blocks(args.chunk_blocks)
-    K = ana.output_length(n_dat)
-    n_out = syn.output_length(K)
+    D = max(1, args.inflight)
+    pairs = []
+    for _ in range(D):
+        ana = pfb.AnalysisPlan(taps, N_CHAN, OS_STR, "polyphase_analysis", n_pol, local)
+        syn = pfb.SynthesisPlan(N_CHAN, OS_STR, NF, OV, True, 1, True, taps, win, None, n_pol, local)
+        if args.chunk_blocks:
+            syn.set_chunk_blocks(args.chunk_blocks)
+        K = ana.output_length(n_dat)
+        n_out = syn.output_length(K)
+        chan_buf = torch.empty((n_pol, K, N_CHAN), dtype=torch.complex64, device=dev)
+        out_buf = torch.empty((n_pol, n_out), dtype=torch.complex64, device=dev)
+        pairs.append((ana, syn, chan_buf, out_buf))
+    ana, syn, chan_buf, out_buf = pairs[0]
 
-    chan_buf = torch.empty((n_pol, K, N_CHAN), dtype=torch.complex64, device=dev)
-    out_buf = torch.empty((n_pol, n_out), dtype=torch.complex64, device=dev)
+    def make_step(ana, syn, chan_buf, out_buf):
+        def step_serial():
+            chan = ana.execute(x)            # (n_pol, K, N) time-major channelised data
+            return syn.execute(chan, layout="ptc")
 
-    def step_serial():
-        chan = ana.execute(x)            # (n_pol, K, N) time-major channelised data
-        return syn.execute(chan, layout="ptc")
+        def step_pipelined():
+            return pfb.roundtrip(ana, syn, x, chan=chan_buf, out=out_buf)
+        return step_pipelined if args.roundtrip else step_serial
 
-    def step_pipelined():
-        return pfb.roundtrip(ana, syn, x, chan=chan_buf, out=out_buf)
-
-    step = step_pipelined if args.roundtrip else step_serial
+    steps_of = [make_step(*p) for p in pairs]
+    step = steps_of[0]
 
     lib = _lib.load()
     if lib.pfb_build_flags() & 1:
         sys.exit(f"bench.py: {_lib.LIB_PATH} is an experiments build (A/B knobs, timing masks); "
                  f"benchmark the release library")
     for _ in range(args.warmup):
-        step()
+        for s in steps_of:
+            s()
     torch.cuda.synchronize(dev)
-    run = step
+    runs = list(steps_of)
     if args.graph:
         # the plans own all their device buffers after the warm-up, so the step is
         # capturable: one graph launch replays the step's kernels
-        graph = torch.cuda.CUDAGraph()
-        cs = torch.cuda.Stream(device=dev)
-        cs.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(cs):
-            step()
-        torch.cuda.current_stream(dev).wait_stream(cs)
-        with torch.cuda.graph(graph):
-            step()
-        torch.cuda.synchronize(dev)
-        run = graph.replay
+        runs = []
+        for s in steps_of:
+            graph = torch.cuda.CUDAGraph()
+            cs = torch.cuda.Stream(device=dev)
+            cs.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(cs):
+                s()
+            torch.cuda.current_stream(dev).wait_stream(cs)
+            with torch.cuda.graph(graph):
+                s()
+            torch.cuda.synchronize(dev)
+            runs.append(graph.replay)
+    if D == 1:
+        run = runs[0]
+    else:
+        # step i on plan pair i mod D and stream i mod D: no dependence between the pairs
+        # (each owns its buffers; the input is read-only), so the GPU may run one step's
+        # analysis beside another's synthesis
+        streams = [torch.cuda.Stream(device=dev) for _ in range(D)]
+        ctr = [0]
+
+        def run():
+            i = ctr[0] % D
+            ctr[0] += 1
+            with torch.cuda.stream(streams[i]):
+                runs[i]()
 
     def sync():
         torch.cuda.synchronize(dev)
@@ -564,6 +592,7 @@ def report(args, res, world, workload, n_pol, n_dat, all_seeds):
                    "parallelism": f"{world} GPU(s) x {n_pol} independent unit(s), one process "
                                   f"per GPU, no collective on the data path",
                    "hip_graph": bool(args.graph),
+                   "steps_in_flight": max(1, args.inflight),
                    "roundtrip_call": bool(args.roundtrip)},
         "roofline": roof,
         "round_trip_hbm_frac": round(rt_gbs / HBM_PEAK_GBS, 4),
