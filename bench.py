@@ -592,7 +592,7 @@ def report(args, res, world, workload, n_pol, n_dat, all_seeds):
                    "parallelism": f"{world} GPU(s) x {n_pol} independent unit(s), one process "
                                   f"per GPU, no collective on the data path",
                    "hip_graph": bool(args.graph),
-                   "steps_in_flight": max(1, args.inflight),
+                   "steps_in_flight": max(1, getattr(args, "inflight", 1)),
                    "roundtrip_call": bool(args.roundtrip)},
         "roofline": roof,
         "round_trip_hbm_frac": round(rt_gbs / HBM_PEAK_GBS, 4),
