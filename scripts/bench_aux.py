@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--skip-mid", action="store_true")
     ap.add_argument("--only-mid", action="store_true")
     ap.add_argument("--only-twostage", action="store_true")
+    ap.add_argument("--inflight", type=int, default=1, help="C3 units in flight (plan pairs/streams)")
     ap.add_argument("--cpu", action="store_true",
                     help="also time the NumPy oracle (1 core) on bounded samples of each config")
     args = ap.parse_args()
@@ -63,7 +64,7 @@ def main():
     if args.cpu:
         cpu_baselines(pfb)
     if args.only_mid:
-        return mid(torch, pfb, noise, dev)
+        return mid(torch, pfb, noise, dev, inflight=args.inflight)
     if args.only_twostage:
         return twostage(torch, pfb, noise, args.reps)
     # ---- C2' (4/3) round trip
@@ -179,19 +180,49 @@ def cpu_baselines(pfb):
         "2^22 samples (2 synthesis blocks)")
 
 
-def mid(torch, pfb, noise, dev, reps=3):
+def mid(torch, pfb, noise, dev, reps=3, inflight=1):
     tm = pfb.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
     nm = 1 << 26
     xm = noise(1, nm)
-    anam = pfb.AnalysisPlan(tm, 4096, "8/7", "polyphase_analysis_padded", 1)
     winm = pfb.PFBWindow().lookup["tukey"](512, 128)
-    synm = pfb.SynthesisPlan(4096, "8/7", 512, 128, True, 1, True, tm, winm, None, 1)
-    Km = anam.output_length(nm)
-    chm = torch.empty((1, Km, 4096), dtype=torch.complex64, device=dev)
-    om = torch.empty((1, synm.output_length(Km)), dtype=torch.complex64, device=dev)
-    ms = timeit(torch, lambda: pfb.roundtrip(anam, synm, xm, chan=chm, out=om), reps)
+    pairs = []
+    for _ in range(max(1, inflight)):
+        anam = pfb.AnalysisPlan(tm, 4096, "8/7", "polyphase_analysis_padded", 1)
+        synm = pfb.SynthesisPlan(4096, "8/7", 512, 128, True, 1, True, tm, winm, None, 1)
+        Km = anam.output_length(nm)
+        chm = torch.empty((1, Km, 4096), dtype=torch.complex64, device=dev)
+        om = torch.empty((1, synm.output_length(Km)), dtype=torch.complex64, device=dev)
+        pairs.append((anam, synm, chm, om))
+    if len(pairs) == 1:
+        anam, synm, chm, om = pairs[0]
+        ms = timeit(torch, lambda: pfb.roundtrip(anam, synm, xm, chan=chm, out=om), reps)
+    else:
+        # D units in flight: unit i on plan pair i mod D and stream i mod D (no dependence
+        # between the pairs), so one unit's FIR / row FFT can run beside another's synthesis
+        streams = [torch.cuda.Stream(dev) for _ in pairs]
+        ctr = [0]
+
+        def step():
+            i = ctr[0] % len(pairs)
+            ctr[0] += 1
+            a, s_, c, o = pairs[i]
+            with torch.cuda.stream(streams[i]):
+                pfb.roundtrip(a, s_, xm, chan=c, out=o)
+
+        def sync_all():
+            torch.cuda.synchronize()
+        for _ in range(len(pairs)):
+            step()
+        sync_all()
+        import time
+        n_it = reps * len(pairs)
+        t0 = time.perf_counter()
+        for _ in range(n_it):
+            step()
+        sync_all()
+        ms = (time.perf_counter() - t0) * 1e3 / n_it
     emit("roundtrip C3 SKA-Mid padded 4096ch", ms, 16 * (1 + 8 / 7) * nm,
-         msamples_per_s=round(nm / ms / 1e3, 1), n_taps=len(tm))
+         msamples_per_s=round(nm / ms / 1e3, 1), n_taps=len(tm), units_in_flight=len(pairs))
 
 
 if __name__ == "__main__":
