@@ -15,6 +15,14 @@ a barrier + device synchronize and the max over ranks is reported;
 value = all ranks' samples / that time.  ``--gpus 1`` is the C2 headline (one
 single-pol unit, seed 100); ``--workload c4`` runs the C4 unit on one GPU too.
 
+Steps in flight (``--inflight D``, default 3): the units are independent, so a rank keeps D
+plan pairs — each with its own stage-1-row scratch, channelised and output buffers — and
+deals step i to pair i mod D on stream i mod D (each step one HIP graph replay).  Every
+step is still one full analysis + synthesis of one unit; the GPU may start a step's
+analysis while another step's synthesis drains, as a streaming pipeline over consecutive
+blocks would.  The timed region is unchanged: K steps between barrier + synchronize.
+The kernel-event region that feeds ``roofline`` runs the steps one at a time (pair 0).
+
 Rank 0 prints one JSON line with the throughput, the roofline of the dominant kernel
 (HIP events on the library's launch stream, algorithmic bytes per launch) and, at N=1,
 the CPU baseline (the NumPy oracle on a bounded sample, on one core and on all the
@@ -66,7 +74,7 @@ def parse():
                          "runs the synthesis channel IFFT on the rows it produces; the "
                          "channelised product is still written in full); 0: separate "
                          "analysis and synthesis calls")
-    ap.add_argument("--inflight", type=int, default=1,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="steps in flight: D plan pairs (each with its own stage-1-row, "
                          "channelised and output buffers) on D streams, step i on pair i mod D, "
                          "so one step's analysis can run beside the previous step's synthesis")

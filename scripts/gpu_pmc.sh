@@ -15,7 +15,7 @@ if [ ${#SETS[@]} -eq 0 ]; then SETS=("FETCH_SIZE" "WRITE_SIZE" \
 for set in "${SETS[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d $ROOT/gpurun_out/pmc_$i -o pmc \
-      -- python3 $ROOT/${PMC_PROG:-bench.py --steps $STEPS --warmup 1 --no-cpu-baseline} ${BENCH_ARGS:-} > $ROOT/gpurun_out/pmc_$i.log 2>&1
+      -- python3 $ROOT/${PMC_PROG:-bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --inflight 1} ${BENCH_ARGS:-} > $ROOT/gpurun_out/pmc_$i.log 2>&1
   rc=$?
   echo "pmc pass $i ($set) rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 $ROOT/gpurun_out/pmc_$i.log; exit $rc; fi

@@ -23,6 +23,6 @@ timeout -k 10 300 python bench.py --steps $STEPS --warmup 3 --workload c4 --no-c
 rc=$?; echo "bench c4 rc=$rc"; cat gpurun_out/bench_c4.json; tail -3 gpurun_out/bench_c4.err
 if [ $rc -ne 0 ]; then exit $rc; fi
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run \
-    -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1
+    -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --inflight 1 > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"
 exit $rc
