@@ -155,6 +155,47 @@ def test_roundtrip_graph_capture(gpu, chunk_blocks):
     assert torch.equal(out, out_ref)
 
 
+def test_roundtrip_steps_in_flight(gpu):
+    """bench.py's in-flight mode: 3 plan pairs, each step one graph replay on its pair's
+    stream, steps dealt round-robin with nothing ordering one pair after another.  Every
+    pair's outputs (channelised product and time series) after 7 overlapping steps on 3
+    different units equal the eager single-stream round trip of that unit bit for bit."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
+    win = pfb.PFBWindow().lookup["tukey"](256, 48)
+    D, n = 3, 1 << 20
+    pairs, refs = [], []
+    for d in range(D):
+        x = _noise_t(torch, gpu, (1, n), 40 + d)
+        ana = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
+        syn = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, 1, 0)
+        c_ref, o_ref = pfb.roundtrip(ana, syn, x)
+        refs.append((c_ref.clone(), o_ref.clone()))
+        chan, out = torch.empty_like(c_ref), torch.empty_like(o_ref)
+        pairs.append((ana, syn, x, chan, out))
+    torch.cuda.synchronize()
+    graphs = []
+    for ana, syn, x, chan, out in pairs:
+        pfb.roundtrip(ana, syn, x, chan=chan, out=out)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            pfb.roundtrip(ana, syn, x, chan=chan, out=out)
+        graphs.append(g)
+        chan.zero_()
+        out.zero_()
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(D)]
+    for i in range(7):
+        with torch.cuda.stream(streams[i % D]):
+            graphs[i % D].replay()
+    torch.cuda.synchronize()
+    for (_, _, _, chan, out), (c_ref, o_ref) in zip(pairs, refs):
+        assert torch.equal(chan, c_ref)
+        assert torch.equal(out, o_ref)
+
+
 # ------------------------------------------------------------------ BASELINE C2 size
 @pytest.fixture(scope="module")
 def c2(gpu):
