@@ -112,12 +112,8 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
   // rows past the last window of the range (the unconditional last prefetch) re-read the
   // last row instead: an L2 hit rather than HBM traffic nobody uses
   const int r_last = (int)(st1 - st0 - 1) * NEW + WIN - 1;
-  // (experiments: timing_mask bit 4 = non-temporal input loads)
-  const bool x_nt = (tmask(a.timing_mask) & 16) != 0;
   auto ld = [&](int r) {  // window row r (relative to row_first)
-    const uint32_t off = (uint32_t)((min(r, r_last) * N + c + shift) * 8);
-    const v2u v = x_nt ? __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 2)
-                       : __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0);
+    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (uint32_t)((min(r, r_last) * N + c + shift) * 8), 0, 0);
     return __builtin_bit_cast(v2f, v);
   };
   // (re, im) as a packed pair: one v_pk_fma_f32 per complex x real tap MAC
@@ -199,12 +195,9 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
           constexpr float n2 = (float)N * (float)N;
           const v2f a0 = acc[s - 1][qq] * n2, a1 = acc[s][qq] * n2;
           // (fused round trip: write-through, the consumer reads them from another CU)
-          const v4u zv = __builtin_bit_cast(v4u, v4f{a0.x, a0.y, a1.x, a1.y});
-        const uint32_t zo = (uint32_t)((((r0 / ZOUT) * N + c) * ZOUT + r0 % ZOUT) * 8);
-        if (!PUB::kOn && (tmask(a.timing_mask) & 64))  // (experiments: non-temporal)
-          __builtin_amdgcn_raw_buffer_store_b128(zv, zb, zo, 0, 2);
-        else
-          __builtin_amdgcn_raw_buffer_store_b128(zv, zb, zo, 0, PUB::kOn ? kSc1 : 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{a0.x, a0.y, a1.x, a1.y}), zb,
+                                                 (uint32_t)((((r0 / ZOUT) * N + c) * ZOUT + r0 % ZOUT) * 8), 0,
+                                                 PUB::kOn ? kSc1 : 0);
         }
       });
     });
@@ -243,9 +236,6 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
                                                          a.sel_split, a.sel_shift, a.sel_n, N, (float)N);
         block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
       }
-    } else if (tmask(a.timing_mask) & 32) {  // (experiments: non-temporal channelised stores)
-      const BufRowStoreNT st{BufRowStore::rows(opol, k0, T, a.row0, a.K, N, (float)N)};
-      block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
     } else {
       const BufRowStore st = BufRowStore::rows(opol, k0, T, a.row0, a.K, N, (float)N);
       block_fft<N, -1, T, NT>(rows, st, rows, tw, c);

@@ -61,15 +61,6 @@ struct BufRowStore {
   }
 };
 
-// BufRowStore with non-temporal stores (experiments build: cache-policy A/B)
-struct BufRowStoreNT {
-  static constexpr bool kIsLds = false;
-  BufRowStore b;
-  __device__ __forceinline__ void store(int row, int c, float2 v) const {
-    const uint32_t off = row >= b.lo ? (uint32_t)((row * b.N + c) * 8) : 0xFFFFFFF0u;
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v, b.scale)), b.r, off, 0, 2);
-  }
-};
 
 // Rows [k0, k0 + T) of a strided channelised product (AnalysisArgs::out_rs): bin c of
 // row `row` at base + row * rs + j(c) * cs, valid rows [lo, hi) and kept bins only — the

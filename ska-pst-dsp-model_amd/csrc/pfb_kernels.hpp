@@ -192,6 +192,9 @@ bool synth_block_supported(int Nf, int W);
 // (pfb_synth_wave.hip); launch_synth_block takes it where it applies
 bool synth_wave_supported(const SynthBlockArgs& a);
 hipError_t launch_synth_wave(const SynthBlockArgs& a, hipStream_t s);
+// Nf = 512, W = 448, keep 256 (SKA-Mid): one output phase per 32 lanes (pfb_synth_wave512.hip)
+bool synth_wave512_supported(const SynthBlockArgs& a);
+hipError_t launch_synth_wave512(const SynthBlockArgs& a, hipStream_t s);
 hipError_t launch_synth_block(const SynthBlockArgs& a, hipStream_t s);
 
 // The SKA-Low round trip as one launch (pfb_roundtrip.hip): nA analysis workgroups (step

@@ -136,9 +136,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     static_for<0, R0>([&](auto r) { x[r] = x[r + DK]; });
     const __amdgpu_buffer_rsrc_t z = make_rsrc(zpol + (int64_t)b * a.keep * N, zbytes);
     static_for<R0, 16>([&](auto r) {
-      const v2u v = (tmask(a.timing_mask) & 16)  // (experiments: non-temporal loads)
-                        ? __builtin_amdgcn_raw_buffer_load_b64(z, zlane, r * N * 16 * 8, 2)
-                        : __builtin_amdgcn_raw_buffer_load_b64(z, zlane, r * N * 16 * 8, SCHED::kLoadAux);
+      const v2u v = __builtin_amdgcn_raw_buffer_load_b64(z, zlane, r * N * 16 * 8, SCHED::kLoadAux);
       x[r] = __builtin_bit_cast(float2, v);
     });
   };
@@ -219,12 +217,8 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       // the discarded t1 < t1_lo, whose negative offsets wrap past 2^31)
       const int base = (t1a < RW) ? ((t1a - a.t1_lo) * N + t0g + col2) * 8 : (int)0x80000000;
       static_for<0, 16>([&](auto t) {
-        if (tmask(a.timing_mask) & 32)  // (experiments: non-temporal stores)
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v[t]), o,
-                                                (uint32_t)(base + t * RW * N * 8), 0, 2);
-        else
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v[t]), o,
-                                                (uint32_t)(base + t * RW * N * 8), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v[t]), o,
+                                              (uint32_t)(base + t * RW * N * 8), 0, 0);
       });
     }
   }

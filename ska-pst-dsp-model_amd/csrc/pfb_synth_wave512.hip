@@ -1,0 +1,283 @@
+// pfb_synth_wave512.hip — synthesis stage 2 for Nf = 512, W = 448 (SKA-Mid at OS 8/7, keep
+// 256: Ov 128) with one output phase per 32 lanes (polyphase_synthesis.m:163-316,
+// re-ordered as DESIGN.md §5 derives; the Nf = 256 counterpart is pfb_synth_wave.hip).
+//
+// Per block b and output phase t0 (one column of the stage-1 rows Z[row][t0]):
+//   Nf-point FFT over time (taper on the way in), keep W bins, x gain x four-step twiddle
+//   (x the output scale), W-point IFFT, overlap-discard.
+// Lane m (< 32) of a phase holds 16 values at every stage:
+//   pass 1   x[m + 32 r] (r < 16)          -> 16-point DFT over r, x w_512^{m f1}
+//   swap 1   lane (f1, h) <- A_{l' + 16 h}[f1], l' < 16  (transpose through the wave's LDS)
+//   pass 2   32-point DFT over m = l' + 16 h by decimation in frequency: one radix-2
+//            butterfly across the lane pair h = 0/1 (DPP quad_perm: lane 2k <-> 2k+1), lane
+//            g = h keeping the bins f2 = 2 f2'' + g, x w_32^{g l'}, 16-point DFT over l'
+//            -> lane g holds the bins f = f1 + 16 (2 f2'' + g), f2'' < 16
+//   select   registers f2'' in [0, 7) and [9, 16) of BOTH lanes are the kept bins; in W-bin
+//            order they are j' = f1 + 16 r'' with r'' = g + 2 k, k < 14 (the W-point IFFT
+//            is 16 x 28 and the lane holds the odd or even half of its 28-point group),
+//            x t4[j'] (lane constants)
+//   pass A   28-point IDFT over r'' by decimation in time: 14-point IDFT over k in
+//            registers, x w_28^{+g t'}, radix-2 across the lane pair -> lane e holds
+//            t1a = t' + 14 e; x e^{+2 pi i f1 t1a / W}
+//   swap 2   (t1a, phase) <- Y_f1[t1a], f1 < 16, across the workgroup
+//   pass B   16-point IDFT over f1          -> y[t1a + 28 t1b], stored when t1 is kept.
+// Both lane-pair butterflies compute self + sigma * partner in one fma per float (sigma = -1
+// on the second lane of the pair); the sign that leaves on that lane's result is folded
+// into its next twiddle table row, so no lane needs a select.
+// A wave holds 2 phases (64 lanes), a 256-thread workgroup 8 adjacent phases; the
+// workgroups of neighbouring phase groups run on the same XCD (64-B halves of every Z
+// and output line).  Every twiddle is a table entry rounded once from double; the gain x
+// twiddle x scale constants come from the plan's tw4s table, once per launch.
+// Register budget: 3 waves per SIMD (<= 168 VGPRs); LDS 47 KB per workgroup (3 per CU).
+#include "pfb_common.hpp"
+
+namespace pfb {
+
+namespace {
+
+constexpr int kW5Threads = 256;
+constexpr int kW5Cols = 8;       // output phases per workgroup
+constexpr int kRowB = 144;       // 16 values + 16 B
+constexpr int kTileB = 2 * 16 * kRowB;  // one phase: swap 1 [f1][h][l'] (f1 stride 288 B),
+                                        // swap 2 [t1a][f1] (rows of 144 B, 28 rows)
+constexpr int kTw1Off = kW5Cols * kTileB;          // [m][f1], 32 rows
+constexpr int kTw32Off = kTw1Off + 32 * kRowB;     // [h][f2'], 2 rows
+constexpr int kRow14B = 112;                       // 14 values
+constexpr int kW28Off = kTw32Off + 2 * kRowB;      // [hi][r_a], 2 rows
+constexpr int kTw2Off = kW28Off + 2 * kRow14B;     // [f1][e][t'], 32 rows
+constexpr int kWinRowB = 80;                       // 16 floats + 16 B
+constexpr int kWinOff = kTw2Off + 32 * kRow14B;    // [m][r], 32 rows
+constexpr int kW5LdsB = kWinOff + 32 * kWinRowB;
+
+__device__ __forceinline__ void lds_pair2(const char* p, float2& a, float2& b) {
+  const v4f q = *reinterpret_cast<const v4f*>(p);
+  a = make_float2(q.x, q.y);
+  b = make_float2(q.z, q.w);
+}
+
+// the value of the other lane of the pair (lane ^ 1)
+__device__ __forceinline__ float pair_swap(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1 /* quad_perm 1,0,3,2 */, 0xF, 0xF,
+                                                 false));
+}
+// self + sg * partner
+__device__ __forceinline__ float2 pair_bfly(float2 a, float sg) {
+  return make_float2(fmaf(pair_swap(a.x), sg, a.x), fmaf(pair_swap(a.y), sg, a.y));
+}
+
+// v[i] *= row[i], i < 2 NP (one ds_read_b128 per pair, multiplied as it arrives)
+template <int NP>
+__device__ __forceinline__ void twiddle_rows(float2* v, const char* row) {
+  static_for<0, NP>([&](auto k) {
+    float2 w0, w1;
+    lds_pair2(row + 16 * k, w0, w1);
+    v[2 * k] = cmul(v[2 * k], w0);
+    v[2 * k + 1] = cmul(v[2 * k + 1], w1);
+  });
+}
+
+}  // namespace
+
+template <bool SPANS>
+__global__ __launch_bounds__(kW5Threads) __attribute__((amdgpu_waves_per_eu(3)))
+void synth_wave512_kernel(SynthBlockArgs a) {
+  constexpr int W = 448, DK = 8;  // keep = 256 rows = 8 register rows of 32
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int N = a.N;
+  const int groups = N / kW5Cols;
+  const int lt = xcd_tile(blockIdx.x, gridDim.x);
+  const int rr = lt / groups;
+  const int Rg = gridDim.x / groups;
+  const int b_begin = (int)((int64_t)a.n_blocks * rr / Rg);
+  const int b_end = (int)((int64_t)a.n_blocks * (rr + 1) / Rg);
+  const int nb = b_end - b_begin;
+  if (nb <= 0) return;  // uniform per workgroup
+  const int t0g = (lt % groups) * kW5Cols;
+  const int pol = blockIdx.y;
+
+  // ---- tables (once per launch)
+  for (int e = tid; e < 512; e += kW5Threads) {
+    const int i = e >> 4, f = e & 15;  // i < 32
+    *reinterpret_cast<float2*>(lds + kTw1Off + i * kRowB + f * 8) = a.twNf[(i * f) & 511];
+    *reinterpret_cast<float*>(lds + kWinOff + i * kWinRowB + f * 4) = a.window[i + 32 * f];
+    if (i < 2) {
+      // pass-2 pair butterfly: lane 1 holds A_hi - A_lo, x -w_32^{l'} = (A_lo - A_hi) w_32^{l'}
+      const float2 w = a.twNf[16 * f];
+      *reinterpret_cast<float2*>(lds + kTw32Off + i * kRowB + f * 8) =
+          i ? make_float2(-w.x, -w.y) : make_float2(1.f, 0.f);
+      if (f < 14) {
+        const float2 v = a.twW[16 * f];  // e^{-2 pi i f / 28}; the inverse takes its conjugate
+        *reinterpret_cast<float2*>(lds + kW28Off + i * kRow14B + f * 8) =
+            i ? make_float2(v.x, -v.y) : make_float2(1.f, 0.f);
+      }
+    }
+  }
+  // W-pass twiddle e^{+2 pi i f1 t1a / W}, t1a = t + 14 e; x -1 on e = 1 (the pass-A pair
+  // butterfly leaves -Y there)
+  for (int e = tid; e < 16 * 2 * 14; e += kW5Threads) {
+    const int f1 = e / 28, q = e % 28, ee = q / 14, t = q % 14;
+    const float2 w = a.twW[(f1 * (t + 14 * ee)) % W];
+    *reinterpret_cast<float2*>(lds + kTw2Off + (2 * f1 + ee) * kRow14B + t * 8) =
+        ee ? make_float2(-w.x, w.y) : make_float2(w.x, -w.y);
+  }
+
+  // lane roles.  Pass 1 / swap-1 writes: phase col = 2 wave + ph, FFT lane m.  Pass 2 to
+  // swap-2 writes: (ph, f1, h) with lane = 32 ph + 2 f1 + h.  Pass B: (col2, t1a).
+  const int ph = lane >> 5;
+  const int m = lane & 31;
+  const int col = 2 * wave + ph;
+  const int h = lane & 1;
+  const int f1 = (lane >> 1) & 15;
+  const float sg = h ? -1.f : 1.f;     // pair butterflies: self + sg * partner
+  const int tile = col * kTileB;
+
+  // ---- lane constants: gain x four-step twiddle x output scale of the lane's kept bins
+  // j' = f1 + 16 (h + 2 k), k < 14
+  float2 t4[14];
+  {
+    const __amdgpu_buffer_rsrc_t tr = make_rsrc(a.tw4s + t0g, (uint32_t)((W - 1) * N + kW5Cols) * 8u);
+    static_for<0, 14>([&](auto k) {
+      const int jp = f1 + 16 * (h + 2 * decltype(k)::value);
+      const v2u x = __builtin_amdgcn_raw_buffer_load_b64(tr, (uint32_t)((jp * N + col) * 8), 0, 0);
+      t4[decltype(k)::value] = __builtin_bit_cast(float2, x);
+    });
+  }
+  __syncthreads();  // tables staged
+
+  const int wr1 = tile + (m >> 4) * kRowB + (m & 15) * 8;  // swap-1 writes (+ f1 * 288)
+  const int rd1 = tile + f1 * (2 * kRowB) + h * kRowB;     // swap-1 reads (+ 16 k)
+  const int wr2 = tile + h * (14 * kRowB) + f1 * 8;        // swap-2 writes (+ t' * 144)
+  const int col2 = lane & 7;
+  const int t1a = wave + 4 * (lane >> 3);                 // valid below 28
+  const int rd2 = col2 * kTileB + min(t1a, 27) * kRowB;   // swap-2 reads (+ 16 k)
+  const char* tw1row = lds + kTw1Off + m * kRowB;
+  const char* tw32row = lds + kTw32Off + h * kRowB;
+  const char* w28row = lds + kW28Off + h * kRow14B;
+  const char* tw2row = lds + kTw2Off + (2 * f1 + h) * kRow14B;
+  const char* winrow = lds + kWinOff + m * kWinRowB;
+
+  const float2* zpol = a.Z + pol * a.z_pol_stride + t0g;
+  const uint32_t zbytes = (tmask(a.timing_mask) & 1) ? 0u : (uint32_t)((511 * N + kW5Cols) * 8);
+  const uint32_t zlane = (uint32_t)((m * N + col) * 8);
+  float2* opol = a.out + pol * a.out_pol_stride;
+
+  float2 x[16];  // raw Z values of the next block, rows m + 32 r
+  auto prefetch = [&](int b, auto reuse) {
+    constexpr int R0 = decltype(reuse)::value ? 16 - DK : 0;
+    static_for<0, R0>([&](auto r) { x[r] = x[r + DK]; });
+    const __amdgpu_buffer_rsrc_t z = make_rsrc(zpol + (int64_t)b * a.keep * N, zbytes);
+    static_for<R0, 16>([&](auto r) {
+      const v2u v = __builtin_amdgcn_raw_buffer_load_b64(z, zlane, r * 32 * N * 8, 0);
+      x[r] = __builtin_bit_cast(float2, v);
+    });
+  };
+  prefetch(b_begin, std::false_type{});
+
+#pragma unroll 1
+  for (int i = 0; i < nb; ++i) {
+    const int b = b_begin + i;
+    // every wave has read the previous block's swap-2 data (from all tiles)
+    __syncthreads();
+    // ---- pass 1: taper, 16-point DFT over r, x w_512^{m f1}
+    float2 v[16];
+    {
+      float wv[16];
+      static_for<0, 4>([&](auto k) {
+        const v4f q = *reinterpret_cast<const v4f*>(winrow + 16 * k);
+        wv[4 * k] = q.x;
+        wv[4 * k + 1] = q.y;
+        wv[4 * k + 2] = q.z;
+        wv[4 * k + 3] = q.w;
+      });
+      static_for<0, 16>([&](auto r) { v[r] = cscale(x[r], wv[r]); });
+    }
+    // the next block's rows (the last block re-reads itself: the wait count stays fixed)
+    prefetch(min(b + 1, b_end - 1), std::true_type{});
+    sdft<16, -1>(v);
+    twiddle_rows<8>(v, tw1row);
+    // ---- swap 1 (inside the wave): A_m[f1] -> tile[f1][m >> 4][m & 15]
+    static_for<0, 16>([&](auto f) {
+      *reinterpret_cast<float2*>(lds + wr1 + decltype(f)::value * (2 * kRowB)) = v[decltype(f)::value];
+    });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 8>([&](auto k) { lds_pair2(lds + rd1 + 16 * k, v[2 * k], v[2 * k + 1]); });
+    // ---- pass 2: radix-2 across the lane pair (m = l' + 16 h), x (-)w_32^{g l'},
+    // 16-point DFT over l'
+    static_for<0, 16>([&](auto l) { v[l] = pair_bfly(v[l], sg); });
+    twiddle_rows<8>(v, tw32row);
+    sdft<16, -1>(v);
+    // ---- kept bins (registers f2'' < 7 and >= 9) x t4, 14-point IDFT over k,
+    // x w_28^{g t'}, radix-2 across the pair, x e^{+2 pi i f1 t1a / W}
+    float2 u[14];
+    static_for<0, 14>([&](auto k) {
+      constexpr int kk = decltype(k)::value;
+      // spans: k < 7 <-> f2'' = k (f < 224), k >= 7 <-> f2'' = k + 2 (f >= 288);
+      // critical: the halves swap (j' = f + 224 / f - 288)
+      constexpr int reg = SPANS ? (kk < 7 ? kk : kk + 2) : (kk < 7 ? kk + 9 : kk - 7);
+      u[kk] = cmul(v[reg], t4[kk]);
+    });
+    sdft<14, +1>(u);
+    twiddle_rows<7>(u, w28row);
+    static_for<0, 14>([&](auto t) { u[t] = pair_bfly(u[t], sg); });
+    twiddle_rows<7>(u, tw2row);
+    // ---- swap 2 (across the workgroup): Y_f1[t1a = t' + 14 e] -> tile[t1a][f1] (the wave's
+    // own swap-1 reads of the tile are issued before these writes)
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 14>([&](auto t) {
+      *reinterpret_cast<float2*>(lds + wr2 + decltype(t)::value * kRowB) = u[decltype(t)::value];
+    });
+    __syncthreads();
+    static_for<0, 8>([&](auto k) { lds_pair2(lds + rd2 + 16 * k, v[2 * k], v[2 * k + 1]); });
+    // ---- pass B: 16-point IDFT over f1 -> t1 = t1a + 28 t1b; overlap-discard on the store
+    sdft<16, +1>(v);
+    {
+      const int64_t ob = (a.block0 + b) * (int64_t)a.Lkeep;  // first kept output sample
+      const int64_t avail = a.out_limit - ob;
+      const int64_t nk = (tmask(a.timing_mask) & 2)
+                             ? 0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
+      const __amdgpu_buffer_rsrc_t o = make_rsrc(opol + ob, (uint32_t)nk * 8u);
+      // lanes t1a >= 28 hold no output: their offsets leave the descriptor's range (as do
+      // the discarded t1 < t1_lo, whose negative offsets wrap past 2^31)
+      int base = (t1a < 28) ? ((t1a - a.t1_lo) * N + t0g + col2) * 8 : (int)0x80000000;
+      // (recomputed every block: 16 hoisted store offsets would not fit the register budget)
+      asm volatile("" : "+v"(base));
+      static_for<0, 16>([&](auto t) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v[t]), o,
+                                              (uint32_t)(base + t * 28 * N * 8), 0, 0);
+      });
+    }
+  }
+}
+
+bool synth_wave512_supported(const SynthBlockArgs& a) {
+  // (32-bit byte offsets: 512 rows x N phases x 8 B per block stay below 2^31)
+  return a.Nf == 512 && a.W == 448 && a.keep == 256 && a.zblk <= 1 && a.N % kW5Cols == 0 &&
+         a.N <= 65536 && a.tw4s != nullptr;
+}
+
+template <bool SPANS>
+static hipError_t launch_w5(const SynthBlockArgs& a, hipStream_t s) {
+  auto kern = synth_wave512_kernel<SPANS>;
+  hipError_t e = set_lds(kern, kW5LdsB);
+  if (e != hipSuccess) return e;
+  const int groups = a.N / kW5Cols;
+  // resident workgroups: 3 per CU; ranges so that the grid is about two rounds of them
+  const int slots = cu_count() * 3;
+  int ranges = std::max(1, (2 * slots + groups * a.n_pol - 1) / (groups * a.n_pol));
+  static const int env_r = knob("PFB_W5_RANGES") ? std::atoi(knob("PFB_W5_RANGES")) : 0;  // A/B
+  if (env_r > 0) ranges = env_r;
+  ranges = std::min(ranges, a.n_blocks);
+  dim3 grid((unsigned)(groups * ranges), (unsigned)a.n_pol);
+  return launch_kernel(kern, grid, dim3(kW5Threads), kW5LdsB, s, a);
+}
+
+hipError_t launch_synth_wave512(const SynthBlockArgs& a, hipStream_t s) {
+  if (a.n_blocks <= 0) return hipSuccess;
+  if (!synth_wave512_supported(a)) return hipErrorInvalidValue;
+  return a.spans ? launch_w5<true>(a, s) : launch_w5<false>(a, s);
+}
+
+}  // namespace pfb

@@ -249,6 +249,20 @@ def test_synthesis_baseline_shapes(gpu, N, os_, nf, ov, blocks):
     assert_pfb_close(got, ref, what=f"synthesis N={N} {os_}")
 
 
+@pytest.mark.parametrize("N", [8, 64])
+@pytest.mark.parametrize("spans", [1, 0])
+@pytest.mark.parametrize("deripple,taper", [(1, "tukey"), (0, "hann"), (1, "top_hat")])
+def test_synthesis_nf512_wave_kernel(gpu, N, spans, deripple, taper):
+    """The SKA-Mid synthesis shape (Nf 512, W 448, Ov 128: synth_wave512_kernel) at small
+    channel counts: spans and critical kept-bin orders, deripple on/off, three tapers, two
+    polarisations, a sample offset and a ragged tail, against the oracle."""
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(N, "8/7", 12)
+    x = _noise(np.random.default_rng(60 + N + 3 * spans), (2, N, 7 * 256 + 256 + 11))
+    got, ref = _synth_case(pfb, x, spans, 512, "8/7", deripple, taps, 128, taper, sample_offset=3)
+    assert_pfb_close(got, ref, what=f"synthesis Nf 512 N={N} spans={spans} dr={deripple} {taper}")
+
+
 @pytest.mark.parametrize("taper,combine", [("tukey", 1), ("hann", 1), ("tukey", 2)])
 def test_synthesis_4096_persistent_chan_ifft(gpu, taper, combine):
     """4096-channel synthesis with more than 2048 channelised rows in one chunk: the
