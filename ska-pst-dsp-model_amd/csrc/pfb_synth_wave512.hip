@@ -38,8 +38,9 @@ namespace {
 constexpr int kW5Threads = 256;
 constexpr int kW5Cols = 8;       // output phases per workgroup
 constexpr int kRowB = 144;       // 16 values + 16 B
-constexpr int kTileB = 2 * 16 * kRowB;  // one phase: swap 1 [f1][h][l'] (f1 stride 288 B),
-                                        // swap 2 [t1a][f1] (rows of 144 B, 28 rows)
+constexpr int kTileB = 2 * 16 * kRowB + 32;  // one phase: swap 1 [f1][h][l'] (f1 stride 288 B),
+                                             // swap 2 rows of 144 B (28 rows); the 32 B
+                                             // put the 8 tiles on different banks
 constexpr int kTw1Off = kW5Cols * kTileB;          // [m][f1], 32 rows
 constexpr int kTw32Off = kTw1Off + 32 * kRowB;     // [h][f2'], 2 rows
 constexpr int kRow14B = 112;                       // 14 values
@@ -78,7 +79,10 @@ __device__ __forceinline__ void twiddle_rows(float2* v, const char* row) {
 
 }  // namespace
 
-template <bool SPANS>
+// XW: pass-1 lanes (phase p, FFT lane m) spread over the workgroup (lane = 8 (m mod 8) + p in
+// wave m / 8): one Z load instruction reads 8 rows x the 8 phases (64-B runs) instead of 32
+// rows x 2 phases, and swap 1 crosses waves (one more workgroup barrier per block)
+template <bool SPANS, bool XW>
 __global__ __launch_bounds__(kW5Threads) __attribute__((amdgpu_waves_per_eu(3)))
 void synth_wave512_kernel(SynthBlockArgs a) {
   constexpr int W = 448, DK = 8;  // keep = 256 rows = 8 register rows of 32
@@ -124,10 +128,11 @@ void synth_wave512_kernel(SynthBlockArgs a) {
         ee ? make_float2(-w.x, w.y) : make_float2(w.x, -w.y);
   }
 
-  // lane roles.  Pass 1 / swap-1 writes: phase col = 2 wave + ph, FFT lane m.  Pass 2 to
-  // swap-2 writes: (ph, f1, h) with lane = 32 ph + 2 f1 + h.  Pass B: (col2, t1a).
+  // lane roles.  Pass 1 / swap-1 writes: phase c1, FFT lane m.  Pass 2 to swap-2 writes:
+  // (ph, f1, h) with lane = 32 ph + 2 f1 + h, phase col = 2 wave + ph.  Pass B: (col2, t1a).
   const int ph = lane >> 5;
-  const int m = lane & 31;
+  const int m = XW ? 8 * wave + (lane >> 3) : lane & 31;
+  const int c1 = XW ? (lane & 7) : 2 * wave + ph;
   const int col = 2 * wave + ph;
   const int h = lane & 1;
   const int f1 = (lane >> 1) & 15;
@@ -147,12 +152,14 @@ void synth_wave512_kernel(SynthBlockArgs a) {
   }
   __syncthreads();  // tables staged
 
-  const int wr1 = tile + (m >> 4) * kRowB + (m & 15) * 8;  // swap-1 writes (+ f1 * 288)
+  const int wr1 = c1 * kTileB + (m >> 4) * kRowB + (m & 15) * 8;  // swap-1 writes (+ f1 * 288)
   const int rd1 = tile + f1 * (2 * kRowB) + h * kRowB;     // swap-1 reads (+ 16 k)
-  const int wr2 = tile + h * (14 * kRowB) + f1 * 8;        // swap-2 writes (+ t' * 144)
+  const int wr2 = tile + h * kRowB + f1 * 8;               // swap-2 writes (+ t' * 288)
+  // swap 2 keeps row t1a = t' + 14 e at row 2 t' + e (the two lanes of a pair write
+  // neighbouring rows: fewer bank conflicts than rows t' and t' + 14)
   const int col2 = lane & 7;
-  const int t1a = wave + 4 * (lane >> 3);                 // valid below 28
-  const int rd2 = col2 * kTileB + min(t1a, 27) * kRowB;   // swap-2 reads (+ 16 k)
+  const int t1a = (lane >> 3) < 7 ? 7 * wave + (lane >> 3) : 28;  // 28: no output (8 lanes a wave)
+  const int rd2 = col2 * kTileB + (t1a < 28 ? 2 * (t1a % 14) + t1a / 14 : 0) * kRowB;  // (+ 16 k)
   const char* tw1row = lds + kTw1Off + m * kRowB;
   const char* tw32row = lds + kTw32Off + h * kRowB;
   const char* w28row = lds + kW28Off + h * kRow14B;
@@ -161,7 +168,7 @@ void synth_wave512_kernel(SynthBlockArgs a) {
 
   const float2* zpol = a.Z + pol * a.z_pol_stride + t0g;
   const uint32_t zbytes = (tmask(a.timing_mask) & 1) ? 0u : (uint32_t)((511 * N + kW5Cols) * 8);
-  const uint32_t zlane = (uint32_t)((m * N + col) * 8);
+  const uint32_t zlane = (uint32_t)((m * N + c1) * 8);
   float2* opol = a.out + pol * a.out_pol_stride;
 
   float2 x[16];  // raw Z values of the next block, rows m + 32 r
@@ -202,7 +209,8 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     static_for<0, 16>([&](auto f) {
       *reinterpret_cast<float2*>(lds + wr1 + decltype(f)::value * (2 * kRowB)) = v[decltype(f)::value];
     });
-    __builtin_amdgcn_wave_barrier();
+    if constexpr (XW) __syncthreads();  // the phase tiles were written by every wave
+    else __builtin_amdgcn_wave_barrier();
     static_for<0, 8>([&](auto k) { lds_pair2(lds + rd1 + 16 * k, v[2 * k], v[2 * k + 1]); });
     // ---- pass 2: radix-2 across the lane pair (m = l' + 16 h), x (-)w_32^{g l'},
     // 16-point DFT over l'
@@ -227,7 +235,7 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     // own swap-1 reads of the tile are issued before these writes)
     __builtin_amdgcn_wave_barrier();
     static_for<0, 14>([&](auto t) {
-      *reinterpret_cast<float2*>(lds + wr2 + decltype(t)::value * kRowB) = u[decltype(t)::value];
+      *reinterpret_cast<float2*>(lds + wr2 + decltype(t)::value * (2 * kRowB)) = u[decltype(t)::value];
     });
     __syncthreads();
     static_for<0, 8>([&](auto k) { lds_pair2(lds + rd2 + 16 * k, v[2 * k], v[2 * k + 1]); });
@@ -258,9 +266,9 @@ bool synth_wave512_supported(const SynthBlockArgs& a) {
          a.N <= 65536 && a.tw4s != nullptr;
 }
 
-template <bool SPANS>
+template <bool SPANS, bool XW>
 static hipError_t launch_w5(const SynthBlockArgs& a, hipStream_t s) {
-  auto kern = synth_wave512_kernel<SPANS>;
+  auto kern = synth_wave512_kernel<SPANS, XW>;
   hipError_t e = set_lds(kern, kW5LdsB);
   if (e != hipSuccess) return e;
   const int groups = a.N / kW5Cols;
@@ -277,7 +285,10 @@ static hipError_t launch_w5(const SynthBlockArgs& a, hipStream_t s) {
 hipError_t launch_synth_wave512(const SynthBlockArgs& a, hipStream_t s) {
   if (a.n_blocks <= 0) return hipSuccess;
   if (!synth_wave512_supported(a)) return hipErrorInvalidValue;
-  return a.spans ? launch_w5<true>(a, s) : launch_w5<false>(a, s);
+  // (PFB_W5_XW=0: pass-1 lanes inside one wave per phase pair, experiments build A/B)
+  static const bool xw = !(knob("PFB_W5_XW") && std::atoi(knob("PFB_W5_XW")) == 0);
+  if (!kExperiments || xw) return a.spans ? launch_w5<true, true>(a, s) : launch_w5<false, true>(a, s);
+  return a.spans ? launch_w5<true, false>(a, s) : launch_w5<false, false>(a, s);
 }
 
 }  // namespace pfb
