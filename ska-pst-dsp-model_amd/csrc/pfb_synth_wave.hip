@@ -37,9 +37,9 @@ bool synth_wave_supported(const SynthBlockArgs& a) {
   return (a.zblk == 1 || a.zblk == 2 || a.zblk == 4) && a.keep == 160;
 }
 
-template <int RW, bool SPANS>
+template <int RW, bool SPANS, bool XW>
 static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
-  auto kern = synth_wave_kernel<RW, SPANS, 10>;
+  auto kern = synth_wave_kernel<RW, SPANS, 10, XW>;
   hipError_t e = set_lds(kern, kLdsB);
   if (e != hipSuccess) return e;
   const int groups = a.N / kCols;
@@ -56,8 +56,15 @@ static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
 hipError_t launch_synth_wave(const SynthBlockArgs& a, hipStream_t s) {
   if (a.n_blocks <= 0) return hipSuccess;
   if (!synth_wave_supported(a)) return hipErrorInvalidValue;
-  if (a.W == 224) return a.spans ? launch_wave_t<14, true>(a, s) : launch_wave_t<14, false>(a, s);
-  return a.spans ? launch_wave_t<12, true>(a, s) : launch_wave_t<12, false>(a, s);
+  // pass-1 lanes spread over the workgroup (synthesis 78.5-80.2 -> 74.2-75.1 us on C2,
+  // profiles/r03_v8_c2_wave_xw_ab.jsonl); PFB_WAVE_XW=0: within the wave (experiments A/B)
+  static const bool xw = !(knob("PFB_WAVE_XW") && std::atoi(knob("PFB_WAVE_XW")) == 0);
+  if (!kExperiments || xw) {
+    if (a.W == 224) return a.spans ? launch_wave_t<14, true, true>(a, s) : launch_wave_t<14, false, true>(a, s);
+    return a.spans ? launch_wave_t<12, true, true>(a, s) : launch_wave_t<12, false, true>(a, s);
+  }
+  if (a.W == 224) return a.spans ? launch_wave_t<14, true, false>(a, s) : launch_wave_t<14, false, false>(a, s);
+  return a.spans ? launch_wave_t<12, true, false>(a, s) : launch_wave_t<12, false, false>(a, s);
 }
 
 }  // namespace pfb

@@ -68,7 +68,11 @@ struct RangeSched {
 
 // DK: overlap reuse, keep = 16 DK (the next block's rows l + 16 r, r < 16 - DK, are this
 // block's registers r + DK).  tg: the workgroup's phase group (16 output phases).
-template <int RW, bool SPANS, int DK, class SCHED>
+// XW: pass-1 lanes (phase p, FFT lane l) spread over the workgroup (lane = 16 (l mod 4) + p
+// in wave l / 4): one Z load instruction reads 2 row pairs x the 16 phases (256-B runs)
+// instead of 8 row pairs x 4 phases (64-B runs), and swap 1 crosses waves (one more
+// workgroup barrier per block)
+template <int RW, bool SPANS, int DK, class SCHED, bool XW = false>
 __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol, int tg, const SCHED& sch) {
   constexpr int W = 16 * RW;
   static_assert(RW <= 14 && RW % 2 == 0, "W = 16 RW with RW even and <= 14");
@@ -113,21 +117,26 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
 
   // swap addresses (lane constants; the row / register offsets are immediates)
   const int wr = col_base(col) + 8 * l;               // swap writes: slot l of rows 0..15
+  // pass 1 (XW: its own lane mapping): FFT lane l1 of phase p1
+  const int l1 = XW ? 4 * wave + (lane >> 4) : l;
+  const int p1 = XW ? (lane & 15) : col;
+  const int wr1 = col_base(p1) + 8 * l1;              // swap-1 writes
   const int rd1 = col_base(col) + l * kRowB;          // swap 1 reads: row l
   const int col2 = lane & 15;                         // pass 3: phase
   const int t1a = wave + 4 * (lane >> 4);             // pass 3: t1a (valid below RW)
   const int rd2 = col_base(col2) + min(t1a, 15) * kRowB;
-  const char* tw1row = lds + kTw1Off + l * kRowB;
+  const char* tw1row = lds + kTw1Off + l1 * kRowB;
   const char* tw2row = lds + kTw2Off + l * kTw2RowB;
-  const char* winrow = lds + kWinOff + l * kWinRowB;
+  const char* winrow = lds + kWinOff + l1 * kWinRowB;
 
   // stage-1 rows in runs of ZB rows per phase (AnalysisArgs::zblk): row ZB g + gi of phase
   // t at Z[(g N + t) ZB + gi]; ZB = 1 is the plain [row][t0] layout.  Row 16 r + l of the
   // block: lane constant + r 16 N (the register's immediate)
   const int ZB = max(a.zblk, 1);
-  const float2* zpol = a.Z + pol * a.z_pol_stride + (int64_t)(t0g + wave * 4) * ZB;
+  const float2* zpol = a.Z + pol * a.z_pol_stride + (int64_t)(t0g + (XW ? 0 : wave * 4)) * ZB;
   const uint32_t zbytes = (tmask(a.timing_mask) & 1) ? 0u : (uint32_t)((16 * 16 * N) * 8);
-  const uint32_t zlane = (uint32_t)((((l / ZB) * N) * ZB + cc * ZB + l % ZB) * 8);
+  const uint32_t zlane = XW ? (uint32_t)((((l1 / ZB) * N) * ZB + p1 * ZB + l1 % ZB) * 8)
+                            : (uint32_t)((((l / ZB) * N) * ZB + cc * ZB + l % ZB) * 8);
   float2* opol = a.out + pol * a.out_pol_stride;
 
   float2 x[16];  // raw Z values of the next block, rows l + 16 r
@@ -175,9 +184,10 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     // ---- swap 1 (inside the wave): element (row f1, slot l) of this phase's tile
     static_for<0, 16>([&](auto f) {
       constexpr int fr = decltype(f)::value;
-      *reinterpret_cast<float2*>(lds + wr + fr * kRowB) = v[fr];
+      *reinterpret_cast<float2*>(lds + wr1 + fr * kRowB) = v[fr];
     });
-    __builtin_amdgcn_wave_barrier();
+    if constexpr (XW) __syncthreads();  // the phase tiles were written by every wave
+    else __builtin_amdgcn_wave_barrier();
     static_for<0, 8>([&](auto k) {
       lds_pair(lds + rd1 + 16 * k, v[2 * k], v[2 * k + 1]);
     });
@@ -224,7 +234,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
   }
 }
 
-template <int RW, bool SPANS, int DK>
+template <int RW, bool SPANS, int DK, bool XW = false>
 __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(3)))
 void synth_wave_kernel(SynthBlockArgs a) {
   const int groups = a.N / kCols;
@@ -233,7 +243,7 @@ void synth_wave_kernel(SynthBlockArgs a) {
   const int Rg = gridDim.x / groups;
   const int b_begin = (int)((int64_t)a.n_blocks * rr / Rg);
   const int b_end = (int)((int64_t)a.n_blocks * (rr + 1) / Rg);
-  synth_wave_body<RW, SPANS, DK>(a, blockIdx.y, lt % groups, RangeSched{b_begin, b_end - b_begin});
+  synth_wave_body<RW, SPANS, DK, RangeSched, XW>(a, blockIdx.y, lt % groups, RangeSched{b_begin, b_end - b_begin});
 }
 
 }  // namespace pfb
