@@ -478,9 +478,10 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
     if lib.pfb_build_flags() & 1:
         sys.exit(f"bench.py: {_lib.LIB_PATH} is an experiments build (A/B knobs, timing masks); "
                  f"benchmark the release library")
-    for _ in range(args.warmup):
-        for s in steps_of:
-            s()
+    # W untimed warm-up steps, dealt over the pairs like the timed ones (a pair that gets
+    # none is still initialised by the eager call that precedes its graph capture)
+    for i in range(args.warmup):
+        steps_of[i % D]()
     torch.cuda.synchronize(dev)
     runs = list(steps_of)
     if args.graph:
