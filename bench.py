@@ -16,12 +16,16 @@ value = all ranks' samples / that time.  ``--gpus 1`` is the C2 headline (one
 single-pol unit, seed 100); ``--workload c4`` runs the C4 unit on one GPU too.
 
 Steps in flight (``--inflight D``, default 3): the units are independent, so a rank keeps D
-plan pairs — each with its own stage-1-row scratch, channelised and output buffers — and
-deals step i to pair i mod D on stream i mod D (each step one HIP graph replay).  Every
-step is still one full analysis + synthesis of one unit; the GPU may start a step's
-analysis while another step's synthesis drains, as a streaming pipeline over consecutive
-blocks would.  The timed region is unchanged: K steps between barrier + synchronize.
-The kernel-event region that feeds ``roofline`` runs the steps one at a time (pair 0).
+plan pairs — each with its own stage-1-row scratch, channelised and output buffers and
+(``--distinct-inputs``, default) its own synthetic units.  With ``--pipeline 1`` (default)
+the K timed steps are one captured two-stream software pipeline: step i's analysis half
+(``pfb_roundtrip_analysis_execute``) on stream A, its synthesis half on stream S after an
+event, step i's analysis waiting for step i-D's synthesis (the pair's rows are free again)
+— so step i+1's analysis runs beside step i's synthesis; ``--pipeline 0`` deals per-step
+graphs round-robin over D streams instead.  Every step is still one full analysis +
+synthesis of one unit.  The timed region is unchanged: the K steps (one replay of the
+captured pipeline) between barrier + synchronize.  The kernel-event region that feeds
+``roofline`` runs the steps one at a time (pair 0).
 
 Rank 0 prints one JSON line with the throughput, the roofline of the dominant kernel
 (HIP events on the library's launch stream, algorithmic bytes per launch) and, at N=1,
@@ -78,6 +82,14 @@ def parse():
                     help="steps in flight: D plan pairs (each with its own stage-1-row, "
                          "channelised and output buffers) on D streams, step i on pair i mod D, "
                          "so one step's analysis can run beside the previous step's synthesis")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="with --inflight D > 1: the K timed steps as one captured two-stream "
+                         "pipeline (pfb_roundtrip_analysis_execute on stream A, "
+                         "pfb_roundtrip_synthesis_execute on stream S, events between); 0: "
+                         "per-step graphs dealt round-robin over D streams")
+    ap.add_argument("--distinct-inputs", type=int, default=1,
+                    help="with --inflight D > 1: every plan pair reads its own synthetic units "
+                         "(seeds + 7919 p), so overlapping steps share no input data")
     ap.add_argument("--kernel-events", type=int, default=1,
                     help="record HIP events around every kernel in the timed region")
     ap.add_argument("--e2e", type=int, default=0,
@@ -439,16 +451,22 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
 
     taps = pfb.design_PFB_FIR_filter(N_CHAN, OS_STR, TAPS_PER_CHAN)
     # independent units: one polarisation series per seed
-    xs = []
-    for sd in seeds:
-        g = torch.Generator(device=dev).manual_seed(sd)
-        xs.append(torch.complex(torch.randn((n_dat,), device=dev, generator=g),
-                                torch.randn((n_dat,), device=dev, generator=g)) / np.sqrt(2.0))
-    x = torch.stack(xs).to(torch.complex64).contiguous()
-    del xs
+    def units(sds):
+        xs = []
+        for sd in sds:
+            g = torch.Generator(device=dev).manual_seed(sd)
+            xs.append(torch.complex(torch.randn((n_dat,), device=dev, generator=g),
+                                    torch.randn((n_dat,), device=dev, generator=g)) / np.sqrt(2.0))
+        return torch.stack(xs).to(torch.complex64).contiguous()
 
     win = pfb.PFBWindow().lookup["tukey"](NF, OV)
     D = max(1, args.inflight)
+    # pair 0 reads the rank's units (seeds above); with --distinct-inputs each further pair
+    # reads its own units (seeds + 7919 p), so steps in flight never share input lines
+    inputs = [units([sd + 7919 * p for sd in seeds]) if (p == 0 or args.distinct_inputs) else None
+              for p in range(D)]
+    inputs = [xi if xi is not None else inputs[0] for xi in inputs]
+    x = inputs[0]
     pairs = []
     for _ in range(D):
         ana = pfb.AnalysisPlan(taps, N_CHAN, OS_STR, "polyphase_analysis", n_pol, local)
@@ -462,7 +480,7 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
         pairs.append((ana, syn, chan_buf, out_buf))
     ana, syn, chan_buf, out_buf = pairs[0]
 
-    def make_step(ana, syn, chan_buf, out_buf):
+    def make_step(ana, syn, chan_buf, out_buf, x):
         def step_serial():
             chan = ana.execute(x)            # (n_pol, K, N) time-major channelised data
             return syn.execute(chan, layout="ptc")
@@ -471,7 +489,7 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
             return pfb.roundtrip(ana, syn, x, chan=chan_buf, out=out_buf)
         return step_pipelined if args.roundtrip else step_serial
 
-    steps_of = [make_step(*p) for p in pairs]
+    steps_of = [make_step(*p, inputs[i]) for i, p in enumerate(pairs)]
     step = steps_of[0]
 
     lib = _lib.load()
@@ -517,8 +535,41 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
     def sync():
         torch.cuda.synchronize(dev)
 
+    batch = None
+    if args.pipeline and args.roundtrip and D > 1:
+        # two-stream software pipeline over the K steps, captured as ONE graph: step i's
+        # analysis half on stream A (after step i-D's synthesis released pair i mod D's
+        # stage-1 rows), its synthesis half on stream S after it — so step i+1's analysis
+        # runs beside step i's synthesis from the first step on
+        def enqueue(k):
+            sa = torch.cuda.current_stream(dev)
+            ss = torch.cuda.Stream(device=dev)
+            ss.wait_stream(sa)
+            ev_a = [torch.cuda.Event() for _ in range(k)]
+            ev_s = [torch.cuda.Event() for _ in range(k)]
+            for i in range(k):
+                p = i % D
+                a_, s_, c_, o_ = pairs[p]
+                if i >= D:
+                    sa.wait_event(ev_s[i - D])
+                pfb.roundtrip_analysis(a_, s_, inputs[p], chan=c_)
+                ev_a[i].record(sa)
+                ss.wait_event(ev_a[i])
+                with torch.cuda.stream(ss):
+                    pfb.roundtrip_synthesis(a_, s_, n_dat, out=o_)
+                ev_s[i].record(ss)
+            sa.wait_stream(ss)
+        pipe = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(pipe):
+            enqueue(args.steps)
+        torch.cuda.synchronize(dev)
+        batch = pipe.replay
+
     # timed region: K steps, no instrumentation (value, ms_per_step)
-    el = timed_region(args.steps, run, world, dist, sync)
+    if batch is not None:
+        el = timed_region(1, batch, world, dist, sync)  # one replay = the K steps
+    else:
+        el = timed_region(args.steps, run, world, dist, sync)
     # profiled region: the same K steps with HIP events recorded around every kernel
     # launch on the library's launch stream (per-kernel durations for the roofline;
     # the events add inter-kernel gaps, so this region is not used for `value`).  The
@@ -602,6 +653,8 @@ def report(args, res, world, workload, n_pol, n_dat, all_seeds):
                                   f"per GPU, no collective on the data path",
                    "hip_graph": bool(args.graph),
                    "steps_in_flight": max(1, getattr(args, "inflight", 1)),
+                   "pipeline": bool(getattr(args, "pipeline", 0)) and max(1, getattr(args, "inflight", 1)) > 1,
+                   "distinct_inputs_per_pair": bool(getattr(args, "distinct_inputs", 1)),
                    "roundtrip_call": bool(args.roundtrip)},
         "roofline": roof,
         "round_trip_hbm_frac": round(rt_gbs / HBM_PEAK_GBS, 4),

@@ -216,6 +216,26 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* analysis, pfb_synthesis_plan
                                  int64_t out_pol_stride, int64_t out_capacity, int64_t* n_out,
                                  void* stream);
 
+/* The fused round trip above in two halves, for a caller that pipelines consecutive
+ * blocks over two streams (block i's synthesis beside block i+1's analysis, each block on
+ * its own plan pair).  pfb_roundtrip_analysis_execute runs the analysis kernel of the
+ * fused path: it writes the channelised product (as pfb_roundtrip_execute does) and the
+ * synthesis stage-1 rows into `synthesis`'s scratch.  pfb_roundtrip_synthesis_execute
+ * turns those rows into the output; n_dat and sample_offset must be the analysis half's.
+ * The halves' results equal pfb_roundtrip_execute's fused path bit for bit.  The caller
+ * orders them (synthesis after the analysis, the next analysis on the same pair after
+ * the synthesis), e.g. with events.  PFB_ERR_UNSUPPORTED when the plans take the chunked
+ * pipeline (see above); PFB_ERR_INVALID_ARG from the synthesis half when no rows of that
+ * size were produced.  Reference: the same lines as pfb_roundtrip_execute. */
+pfb_status pfb_roundtrip_analysis_execute(pfb_analysis_plan* analysis, pfb_synthesis_plan* synthesis,
+                                          const pfb_cf32* in, int64_t in_pol_stride, int64_t n_dat,
+                                          pfb_cf32* chan, int64_t chan_pol_stride, int64_t chan_capacity,
+                                          int64_t* n_chan_rows, int64_t sample_offset, void* stream);
+pfb_status pfb_roundtrip_synthesis_execute(pfb_analysis_plan* analysis, pfb_synthesis_plan* synthesis,
+                                           int64_t n_dat, int64_t sample_offset, pfb_cf32* out,
+                                           int64_t out_pol_stride, int64_t out_capacity, int64_t* n_out,
+                                           void* stream);
+
 /* Round-trip output length estimate — replaces calc_output_nbins(nbins, channels,
  * os_factor, filter_taps, input_fft_length, input_overlap) (calc_output_nbins.m:17-27):
  * Matlab double arithmetic with its floor()s, so a non-integral normalize(os, n) gives the

@@ -1415,12 +1415,15 @@ static pfb_status roundtrip_one_launch(pfb_analysis_plan* pa, pfb_synthesis_plan
 }
 #endif  // PFB_EXPERIMENTS
 
-pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, const pfb_cf32* in,
-                                 int64_t in_ps, int64_t n_dat, pfb_cf32* chan, int64_t chan_ps,
-                                 int64_t chan_cap, int64_t* n_chan_rows, int64_t sample_offset,
-                                 pfb_cf32* out, int64_t out_ps, int64_t out_cap, int64_t* n_out,
-                                 void* stream) {
-  if (!pa || !ps || (!in && n_dat > 0)) return fail(PFB_ERR_INVALID_ARG, "null argument");
+// phase 0: the whole round trip; 1 / 2: only the analysis / only the synthesis half of the
+// fused path (pfb_roundtrip_analysis_execute / pfb_roundtrip_synthesis_execute), which hand
+// the stage-1 rows over in the synthesis plan's scratch
+static pfb_status roundtrip_run(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, const pfb_cf32* in,
+                                int64_t in_ps, int64_t n_dat, pfb_cf32* chan, int64_t chan_ps,
+                                int64_t chan_cap, int64_t* n_chan_rows, int64_t sample_offset,
+                                pfb_cf32* out, int64_t out_ps, int64_t out_cap, int64_t* n_out,
+                                void* stream, int phase) {
+  if (!pa || !ps || (!in && n_dat > 0 && phase != 2)) return fail(PFB_ERR_INVALID_ARG, "null argument");
   if (pa->device != ps->device) return fail(PFB_ERR_INVALID_ARG, "plans on different devices");
   if (pa->variant == pfb::kLowCbf)
     return fail(PFB_ERR_UNSUPPORTED, "round trip of the LowCBF filterbank: use the separate calls");
@@ -1438,16 +1441,22 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
   if (n_chan_rows) *n_chan_rows = K;
   if (n_out) *n_out = olen;
   if (K == 0) return PFB_OK;
-  if (!chan || (olen > 0 && !out)) return fail(PFB_ERR_INVALID_ARG, "null output");
-  if (chan_cap < K) return fail(PFB_ERR_BUFFER_TOO_SMALL, "channelised capacity %lld < %lld rows",
-                                (long long)chan_cap, (long long)K);
-  if (out_cap < olen) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld",
-                                  (long long)out_cap, (long long)olen);
-  if (in_ps < n_dat || chan_ps < K * pa->N || (olen > 0 && out_ps < olen))
-    return fail(PFB_ERR_INVALID_ARG, "polarisation stride smaller than the data");
+  if (phase != 2) {
+    if (!chan) return fail(PFB_ERR_INVALID_ARG, "null output");
+    if (chan_cap < K) return fail(PFB_ERR_BUFFER_TOO_SMALL, "channelised capacity %lld < %lld rows",
+                                  (long long)chan_cap, (long long)K);
+    if (in_ps < n_dat || chan_ps < K * pa->N)
+      return fail(PFB_ERR_INVALID_ARG, "polarisation stride smaller than the data");
+  }
+  if (phase != 1) {
+    if (olen > 0 && !out) return fail(PFB_ERR_INVALID_ARG, "null output");
+    if (out_cap < olen) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld",
+                                    (long long)out_cap, (long long)olen);
+    if (olen > 0 && out_ps < olen) return fail(PFB_ERR_INVALID_ARG, "polarisation stride smaller than the data");
+  }
   const float2* x = (const float2*)in;
   float2* y = (float2*)chan;
-  if (B == 0) return analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s);
+  if (B == 0) return phase == 2 ? PFB_OK : analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s);
 
   // Fused: the analysis kernel also writes the synthesis stage-1 rows (the channel IFFT
   // of every row it produces, taken as N^2 x its FIR sums before the FFT rather than from
@@ -1474,7 +1483,11 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
   const size_t zbytes = (size_t)pa->n_pol * zrows * pa->N * sizeof(float2);
   bool fuse = !no_fuse && analysis_emits_z(pa) && ps->identity_perm && !ps->has_cgain &&
               !ps->has_spectral && ps->chunk_blocks <= 0 && zbytes <= ((size_t)16 << 30);
-  if (fuse) {
+  if (fuse && phase == 2) {
+    // the synthesis half reads the rows the analysis half left in the plan's scratch
+    if (!ps->Z.p || ps->Z.bytes < zbytes)
+      return fail(PFB_ERR_INVALID_ARG, "split round trip: no stage-1 rows of this size (run the analysis half first)");
+  } else if (fuse) {
     // the rows of the whole call stay resident; a device without room for them takes the
     // chunked pipeline below (its scratch is one chunk's rows) instead of failing
     const hipError_t ze = ps->Z.ensure(zbytes);
@@ -1484,6 +1497,15 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
     } else if (ze != hipSuccess) {
       return fail(PFB_ERR_HIP, "round trip stage-1 rows (%zu bytes): %s", zbytes, hipGetErrorString(ze));
     }
+  }
+  if (phase != 0) {
+    // the split round trip exists for the fused path only (one scratch of rows handed over)
+    if (!fuse) return fail(PFB_ERR_UNSUPPORTED, "split round trip: these plans take the chunked pipeline "
+                                                "(use pfb_roundtrip_execute)");
+    float2* Z = ps->Z.as<float2>();
+    if (phase == 1)
+      return analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0, nullptr, zblk);
+    return synthesis_blocks(ps, Z + (off - z0) * pa->N, zrows * pa->N, 0, B, (float2*)out, out_ps, olen, s, zblk);
   }
 #ifdef PFB_EXPERIMENTS
   if (fuse && zblk == 2) {
@@ -1568,6 +1590,30 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, 
   HIPCHK(hipEventRecord(pa->events[1 + n_chunks], pa->aux));
   HIPCHK(hipStreamWaitEvent(s, pa->events[1 + n_chunks], 0));
   return PFB_OK;
+}
+
+pfb_status pfb_roundtrip_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, const pfb_cf32* in,
+                                 int64_t in_ps, int64_t n_dat, pfb_cf32* chan, int64_t chan_ps,
+                                 int64_t chan_cap, int64_t* n_chan_rows, int64_t sample_offset,
+                                 pfb_cf32* out, int64_t out_ps, int64_t out_cap, int64_t* n_out,
+                                 void* stream) {
+  return roundtrip_run(pa, ps, in, in_ps, n_dat, chan, chan_ps, chan_cap, n_chan_rows, sample_offset,
+                       out, out_ps, out_cap, n_out, stream, 0);
+}
+
+pfb_status pfb_roundtrip_analysis_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, const pfb_cf32* in,
+                                          int64_t in_ps, int64_t n_dat, pfb_cf32* chan, int64_t chan_ps,
+                                          int64_t chan_cap, int64_t* n_chan_rows, int64_t sample_offset,
+                                          void* stream) {
+  return roundtrip_run(pa, ps, in, in_ps, n_dat, chan, chan_ps, chan_cap, n_chan_rows, sample_offset,
+                       nullptr, 0, 0, nullptr, stream, 1);
+}
+
+pfb_status pfb_roundtrip_synthesis_execute(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, int64_t n_dat,
+                                           int64_t sample_offset, pfb_cf32* out, int64_t out_ps,
+                                           int64_t out_cap, int64_t* n_out, void* stream) {
+  return roundtrip_run(pa, ps, nullptr, n_dat, n_dat, nullptr, 0, 0, nullptr, sample_offset, out, out_ps,
+                       out_cap, n_out, stream, 2);
 }
 
 // ------------------------------------------------------------------ utilities

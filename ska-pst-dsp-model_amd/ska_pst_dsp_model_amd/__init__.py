@@ -11,7 +11,8 @@ from ._lib import PfbError, device_count
 from .config import Rational, default_config, load_config
 from .core import (AnalysisPlan, SynthesisPlan, polyphase_analysis, polyphase_analysis_padded,
                    polyphase_analysis_lowcbf,
-                   polyphase_synthesis, roundtrip, calc_output_nbins)
+                   polyphase_synthesis, roundtrip, roundtrip_analysis, roundtrip_synthesis,
+                   calc_output_nbins)
 from .filterbank import (Channelizer, DeChannelizer, FilterBank, InverseFilterBank,
                          TwoStageFilterBank, TwoStageInverseFilterBank)
 from .firio import (design_PFB_FIR_filter, design_PFB_FIR_filter_two_stage,
@@ -25,6 +26,7 @@ __all__ = [
     "SynthesisPlan", "polyphase_analysis", "polyphase_analysis_padded", "polyphase_analysis_lowcbf", "polyphase_synthesis",
     "Channelizer", "DeChannelizer", "FilterBank", "InverseFilterBank", "TwoStageFilterBank",
     "TwoStageInverseFilterBank", "design_PFB_FIR_filter", "design_PFB_FIR_filter_two_stage",
-    "read_fir_filter_coeff", "PFBWindow", "identity_taper", "roundtrip", "calc_output_nbins",
+    "read_fir_filter_coeff", "PFBWindow", "identity_taper", "roundtrip", "roundtrip_analysis",
+    "roundtrip_synthesis", "calc_output_nbins",
     "sgcht", "PureTone", "Impulse", "TestPureTone", "TestImpulse",
 ]

@@ -99,6 +99,11 @@ SYMBOLS = [
     ("pfb_roundtrip_execute", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                         c_void_p, c_int64, c_int64, POINTER(c_int64), c_int64,
                                         c_void_p, c_int64, c_int64, POINTER(c_int64), c_void_p]),
+    ("pfb_roundtrip_analysis_execute", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64,
+                                                 c_void_p, c_int64, c_int64, POINTER(c_int64),
+                                                 c_int64, c_void_p]),
+    ("pfb_roundtrip_synthesis_execute", c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p,
+                                                  c_int64, c_int64, POINTER(c_int64), c_void_p]),
     ("pfb_dada_unpack", c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int64, c_int32,
                                   c_int32, c_void_p, c_int64, c_void_p]),
     ("pfb_dada_pack", c_int32, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_int32,

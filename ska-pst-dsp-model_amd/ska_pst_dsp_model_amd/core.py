@@ -378,6 +378,55 @@ def roundtrip(analysis: AnalysisPlan, synthesis: SynthesisPlan, x, sample_offset
     return chan, out
 
 
+def roundtrip_analysis(analysis: AnalysisPlan, synthesis: SynthesisPlan, x, sample_offset: int = 1,
+                       chan=None):
+    """The analysis half of the fused round trip (``pfb_roundtrip_analysis_execute``):
+    writes the channelised product (returned, as ``roundtrip``'s ``chan``) and leaves the
+    synthesis stage-1 rows in ``synthesis``'s scratch for ``roundtrip_synthesis``.  For
+    pipelining consecutive blocks over two streams (each block on its own plan pair);
+    the caller orders the halves.  ``PfbError`` (unsupported) when the plans take the
+    chunked pipeline."""
+    x, dev = analysis._prep_in(x)
+    if not dev:
+        raise ValueError("roundtrip_analysis() takes device tensors")
+    t = _torch()
+    n_pol, n_dat = x.shape
+    if n_pol != analysis.n_pol or n_pol != synthesis.n_pol:
+        raise ValueError(f"plans built for n_pol={analysis.n_pol}/{synthesis.n_pol}, got {n_pol}")
+    K = analysis.output_length(n_dat)
+    if chan is None:
+        chan = t.empty((n_pol, max(K, 0), analysis.n_chan), dtype=t.complex64, device=x.device)
+    if tuple(chan.shape) != (n_pol, K, analysis.n_chan):
+        raise ValueError("preallocated chan has the wrong shape")
+    kr = c_int64(0)
+    _lib.check(_lib.load().pfb_roundtrip_analysis_execute(
+        analysis._h, synthesis._h, c_void_p(x.data_ptr()), n_dat, n_dat,
+        c_void_p(chan.data_ptr()), K * analysis.n_chan, K, byref(kr), int(sample_offset), _stream_of(x)))
+    return chan
+
+
+def roundtrip_synthesis(analysis: AnalysisPlan, synthesis: SynthesisPlan, n_dat: int,
+                        sample_offset: int = 1, out=None, device=None):
+    """The synthesis half (``pfb_roundtrip_synthesis_execute``) of a
+    ``roundtrip_analysis`` call with the same ``n_dat`` / ``sample_offset``: returns the
+    (n_pol, n_out) series, equal to ``roundtrip``'s ``out`` bit for bit.  Runs on the
+    current stream of ``out``'s device (or ``device``)."""
+    t = _torch()
+    n_pol = synthesis.n_pol
+    K = analysis.output_length(int(n_dat))
+    n_out = synthesis.output_length(max(K - (int(sample_offset) - 1), 0))
+    if out is None:
+        dv = t.device("cuda", synthesis.device if device is None else device)
+        out = t.empty((n_pol, max(n_out, 0)), dtype=t.complex64, device=dv)
+    if tuple(out.shape) != (n_pol, n_out):
+        raise ValueError("preallocated out has the wrong shape")
+    no = c_int64(0)
+    _lib.check(_lib.load().pfb_roundtrip_synthesis_execute(
+        analysis._h, synthesis._h, int(n_dat), int(sample_offset), c_void_p(out.data_ptr()),
+        max(n_out, 1), n_out, byref(no), _stream_of(out)))
+    return out
+
+
 # ============================================================================ helpers
 def calc_output_nbins(nbins, channels, os_factor, filter_taps, input_fft_length, input_overlap):
     """calc_output_nbins.m:1-28 (same arguments: ``os_factor`` a Rational / "nu/de" / Matlab

@@ -196,6 +196,45 @@ def test_roundtrip_steps_in_flight(gpu):
         assert torch.equal(out, o_ref)
 
 
+@pytest.mark.parametrize("N,nf,ov,variant", [
+    (256, 256, 48, "polyphase_analysis"),           # streaming analysis + wave synthesis
+    (512, 512, 128, "polyphase_analysis_padded"),   # register-window FIR + row FFT + wave512
+])
+def test_roundtrip_split_halves(gpu, N, nf, ov, variant):
+    """pfb_roundtrip_analysis_execute + pfb_roundtrip_synthesis_execute (the halves bench.py
+    pipelines over two streams) equal pfb_roundtrip_execute bit for bit — also when the
+    halves run on two streams ordered by an event; the synthesis half of a fresh plan (no
+    rows yet) and the halves of a chunked plan are rejected."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(N, "8/7", 12)
+    x = _noise_t(torch, gpu, (2, 1 << 20), 17)
+    win = pfb.PFBWindow().lookup["tukey"](nf, ov)
+
+    def plans():
+        return (pfb.AnalysisPlan(taps, N, "8/7", variant, 2, 0),
+                pfb.SynthesisPlan(N, "8/7", nf, ov, True, 1, True, taps, win, None, 2, 0))
+    ana, syn = plans()
+    c_ref, o_ref = pfb.roundtrip(ana, syn, x, sample_offset=1)
+    c_ref, o_ref = c_ref.clone(), o_ref.clone()
+    ana2, syn2 = plans()
+    with pytest.raises(pfb.PfbError):
+        pfb.roundtrip_synthesis(ana2, syn2, x.shape[1], device=gpu.index or 0)
+    chan = pfb.roundtrip_analysis(ana2, syn2, x)
+    sa, ss = torch.cuda.current_stream(), torch.cuda.Stream()
+    ev = torch.cuda.Event()
+    ev.record(sa)
+    ss.wait_event(ev)
+    with torch.cuda.stream(ss):
+        out = pfb.roundtrip_synthesis(ana2, syn2, x.shape[1], device=gpu.index or 0)
+    torch.cuda.synchronize()
+    assert torch.equal(chan, c_ref)
+    assert torch.equal(out, o_ref)
+    syn2.set_chunk_blocks(2)
+    with pytest.raises(pfb.PfbError):
+        pfb.roundtrip_analysis(ana2, syn2, x)
+
+
 # ------------------------------------------------------------------ BASELINE C2 size
 @pytest.fixture(scope="module")
 def c2(gpu):
