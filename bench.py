@@ -595,6 +595,37 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
                               "alg_bytes_per_launch": by.value / nl.value,
                               "ms_per_step": ms.value / args.steps}
 
+    # Kernel durations for the roofline: each kernel of the step launched K times back to back
+    # on the current stream (the split round trip's halves on pair 0; the library launches on
+    # torch's current stream, so torch events bracket exactly these launches) — the average
+    # is the kernel plus the gap between two dispatches.  The per-launch event pairs above
+    # also bracket each dispatch's end-of-kernel release and read ≈ 5 µs longer than a
+    # rocprofv3 kernel trace; they stay in the line as "event_bracketed".
+    if args.roundtrip and args.kernel_events and kern:
+        a0, s0, c0, o0 = pairs[0]
+        x0 = inputs[0]
+
+        def batch_ms(fn):
+            fn()
+            torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.steps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize(dev)
+            return e0.elapsed_time(e1) / args.steps
+        try:
+            t_a = batch_ms(lambda: pfb.roundtrip_analysis(a0, s0, x0, chan=c0))
+            t_s = batch_ms(lambda: pfb.roundtrip_synthesis(a0, s0, n_dat, out=o0))
+        except pfb.PfbError:
+            t_a = t_s = None
+        for key, t in (("analysis+chan_ifft", t_a), ("synth_block", t_s)):
+            if t is not None and key in kern:
+                kern[key]["event_bracketed_avg_ms"] = kern[key]["avg_ms"]
+                kern[key]["avg_ms"] = t
+                kern[key]["timing"] = f"{args.steps} launches back to back between two HIP events"
+
     copy_gbs = copy_rate(torch, dev, lib) if rank == 0 else None
 
     e2e = None

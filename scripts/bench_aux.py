@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--only-mid", action="store_true")
     ap.add_argument("--only-twostage", action="store_true")
     ap.add_argument("--inflight", type=int, default=1, help="C3 units in flight (plan pairs/streams)")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="with --inflight > 1: the split round trip pipelined over two streams")
     ap.add_argument("--cpu", action="store_true",
                     help="also time the NumPy oracle (1 core) on bounded samples of each config")
     args = ap.parse_args()
@@ -64,7 +66,7 @@ def main():
     if args.cpu:
         cpu_baselines(pfb)
     if args.only_mid:
-        return mid(torch, pfb, noise, dev, inflight=args.inflight)
+        return mid(torch, pfb, noise, dev, inflight=args.inflight, pipeline=bool(args.pipeline))
     if args.only_twostage:
         return twostage(torch, pfb, noise, args.reps)
     # ---- C2' (4/3) round trip
@@ -180,7 +182,7 @@ def cpu_baselines(pfb):
         "2^22 samples (2 synthesis blocks)")
 
 
-def mid(torch, pfb, noise, dev, reps=3, inflight=1):
+def mid(torch, pfb, noise, dev, reps=3, inflight=1, pipeline=False):
     tm = pfb.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
     nm = 1 << 26
     xm = noise(1, nm)
@@ -196,6 +198,39 @@ def mid(torch, pfb, noise, dev, reps=3, inflight=1):
     if len(pairs) == 1:
         anam, synm, chm, om = pairs[0]
         ms = timeit(torch, lambda: pfb.roundtrip(anam, synm, xm, chan=chm, out=om), reps)
+    elif pipeline:
+        # the split round trip as a two-stream pipeline (bench.py --pipeline): unit i's
+        # FIR + row FFT on stream A beside unit i-1's synthesis on stream S
+        for a, s_, c, o in pairs:
+            pfb.roundtrip(a, s_, xm, chan=c, out=o)
+        torch.cuda.synchronize()
+        D = len(pairs)
+
+        def enqueue(k):
+            sa = torch.cuda.current_stream()
+            ss = torch.cuda.Stream(dev)
+            ss.wait_stream(sa)
+            ev_a = [torch.cuda.Event() for _ in range(k)]
+            ev_s = [torch.cuda.Event() for _ in range(k)]
+            for i in range(k):
+                a, s_, c, o = pairs[i % D]
+                if i >= D:
+                    sa.wait_event(ev_s[i - D])
+                pfb.roundtrip_analysis(a, s_, xm, chan=c)
+                ev_a[i].record(sa)
+                ss.wait_event(ev_a[i])
+                with torch.cuda.stream(ss):
+                    pfb.roundtrip_synthesis(a, s_, nm, out=o)
+                ev_s[i].record(ss)
+            sa.wait_stream(ss)
+        import time
+        n_it = reps * D
+        enqueue(D)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        enqueue(n_it)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3 / n_it
     else:
         # D units in flight: unit i on plan pair i mod D and stream i mod D (no dependence
         # between the pairs), so one unit's FIR / row FFT can run beside another's synthesis
@@ -222,7 +257,8 @@ def mid(torch, pfb, noise, dev, reps=3, inflight=1):
         sync_all()
         ms = (time.perf_counter() - t0) * 1e3 / n_it
     emit("roundtrip C3 SKA-Mid padded 4096ch", ms, 16 * (1 + 8 / 7) * nm,
-         msamples_per_s=round(nm / ms / 1e3, 1), n_taps=len(tm), units_in_flight=len(pairs))
+         msamples_per_s=round(nm / ms / 1e3, 1), n_taps=len(tm), units_in_flight=len(pairs),
+         pipeline=bool(pipeline and len(pairs) > 1))
 
 
 if __name__ == "__main__":
