@@ -118,8 +118,21 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
   };
   // (re, im) as a packed pair: one v_pk_fma_f32 per complex x real tap MAC
   v2f win[WIN];
+  if (a.pre != nullptr && g0 < 0) {
+    // a stream object's carried samples in front of the input: window sample (row i, column
+    // c) is sample (row_first + i) N + c of the carry-then-input series; below pad it is
+    // pre[pol][...], at or above it the input (each range-checked load returns 0 outside
+    // its part, so the sum is the one sample)
+    const __amdgpu_buffer_rsrc_t pr = make_rsrc(a.pre + pol * a.pre_pol_stride, (uint32_t)(a.pad * 8));
 #pragma unroll
-  for (int i = 0; i < WIN; ++i) win[i] = ld(i);
+    for (int i = 0; i < WIN; ++i) {
+      const v2u pv = __builtin_amdgcn_raw_buffer_load_b64(pr, (uint32_t)(((row_first + i) * N + c) * 8), 0, 0);
+      win[i] = ld(i) + __builtin_bit_cast(v2f, pv);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < WIN; ++i) win[i] = ld(i);
+  }
 
   // LDS: twiddles behind the FFT rows, then F = [N zeros, taps, zeros]
   float* F = reinterpret_cast<float*>(smem) + SH::F_OFF;

@@ -241,13 +241,13 @@ struct OutLayout {
 static pfb::AnalysisArgs analysis_args(const pfb_analysis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
                                        float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
                                        int64_t K_total, float2* z, int64_t z_ps, int64_t z_row0, int64_t pad,
-                                       const OutLayout* lay, int zblk);
+                                       const OutLayout* lay, int zblk, const float2* pre = nullptr);
 
 static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
                                float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
                                int64_t K_total, hipStream_t s, float2* z = nullptr,
                                int64_t z_ps = 0, int64_t z_row0 = 0, int64_t pad = 0,
-                               const OutLayout* lay = nullptr, int zblk = 0) {
+                               const OutLayout* lay = nullptr, int zblk = 0, const float2* pre = nullptr) {
   if (K_end <= row0) return PFB_OK;
   if (p->variant == pfb::kLowCbf) {
     pfb::LowCbfArgs l{};
@@ -267,7 +267,7 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
     return PFB_OK;
   }
   pfb::AnalysisArgs a = analysis_args(p, in, in_ps, n_dat, out, out_ps, row0, K_end, K_total, z, z_ps, z_row0,
-                                      pad, lay, zblk);
+                                      pad, lay, zblk, pre);
   a.scratch = nullptr;
   if (!p->fused && !z) {
     HIPCHK(p->scratch.ensure((size_t)p->n_pol * (K_end - row0) * p->N * sizeof(float2)));
@@ -289,8 +289,10 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
 static pfb::AnalysisArgs analysis_args(const pfb_analysis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
                                        float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
                                        int64_t K_total, float2* z, int64_t z_ps, int64_t z_row0, int64_t pad,
-                                       const OutLayout* lay, int zblk) {
+                                       const OutLayout* lay, int zblk, const float2* pre) {
   pfb::AnalysisArgs a{};
+  a.pre = pre;        // the pad samples in front of `in` (stream carry); null: zeros
+  a.pre_pol_stride = pad;
   a.z = z;
   a.z_pol_stride = z_ps;
   a.z_row0 = z_row0;
@@ -579,6 +581,22 @@ static pfb_status filterbank_exec(pfb_analysis_plan* p, const pfb_cf32* in, int6
       if (Kt > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld rows",
                                 (long long)cap, (long long)Kt);
       const int64_t M = p->M, PN = (int64_t)p->P * p->N;
+      if (B <= PN) {
+        // ONE launch: the streaming kernel reads the carried samples through a second
+        // descriptor in its first window (AnalysisArgs::pre) — no stitched rows, no copies
+        // before it; then the new carry (stream order: after the kernel read the old one)
+        pfb_status st = analysis_run(p, (const float2*)in, in_ps, n_in, (float2*)out, out_ps, 0, Kt, K, s,
+                                     nullptr, 0, 0, B, lay, 0, p->carry.as<float2>());
+        if (st != PFB_OK) return st;
+        const int64_t nb = total - input_idat;
+        if (nb > 0) {
+          HIPCHK(p->carry.ensure((size_t)p->n_pol * nb * sizeof(float2)));
+          HIPCHK(copy_pols(p->carry.as<float2>(), nb, (const float2*)in + (input_idat - B), in_ps, nb,
+                           p->n_pol, hipMemcpyDeviceToDevice, s));
+        }
+        p->buffered = std::max<int64_t>(nb, 0);
+        return PFB_OK;
+      }
       const int64_t k_split = std::min(Kt, (B + M - 1) / M);
       if (k_split > 0) {
         const int64_t L = std::min(total, (k_split - 1) * M + PN);

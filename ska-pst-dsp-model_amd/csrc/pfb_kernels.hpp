@@ -61,6 +61,11 @@ struct AnalysisArgs {
   // leading zeros in front of `in` (the LowCBF wrapper's one-time pre-padding) — the
   // streaming kernel reads x[r N + c - pad] (zero for negative indices); 0 otherwise
   int64_t pad;
+  // with pad > 0: the pad samples in front of `in` are pre[pol][0, pad) (a stream object's
+  // carried samples; null: zeros, the LowCBF pre-padding).  Streaming kernel only, read by the
+  // first workgroup's first window (the launcher checks pad <= the window's samples)
+  const float2* pre;
+  int64_t pre_pol_stride;
   float lcbf_scale;  // LowCBF streaming path: output scale (2^12)
   // Strided channelised output (streaming kernel only, out_rs > 0): bin c of row k goes to
   // out[pol][k * out_rs + j * out_cs] with j = c (sel_n = 0) or the two-stage chomp
