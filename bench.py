@@ -330,6 +330,13 @@ def resolve_workload(args, world: int) -> str:
     return "c2" if world == 1 else "c4"
 
 
+def pair_seeds(seeds, inflight: int, distinct: bool):
+    """Seeds of every unit a rank's timed region processes: plan pair p (of the D steps in
+    flight) reads units seeds + 7919 p with --distinct-inputs, else pair 0's units."""
+    D = max(1, inflight)
+    return [sd + (7919 * p if distinct else 0) for p in range(D) for sd in seeds]
+
+
 def rank_units(workload: str, rank: int):
     """Seeds of the independent units (one per polarisation) rank `rank` processes:
     C2 one single-pol unit (seed 100 + rank); C4 one dual-pol DADA time block = 2 units,
@@ -386,7 +393,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         res = run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds)
 
-    all_seeds = gather_seeds(dist, world, seeds, args.stub_device, torch, local)
+    all_seeds = gather_seeds(dist, world, pair_seeds(seeds, args.inflight, args.distinct_inputs),
+                             args.stub_device, torch, local)
     if rank == 0:
         out = report(args, res, world, workload, n_pol, n_dat, all_seeds)
         out["cpu_baseline"] = cpu
@@ -438,8 +446,8 @@ def run_stub(args, world, dist):
     for _ in range(args.warmup):
         step()
     el = timed_region(args.steps, step, world, dist, lambda: None)
-    return {"el": el, "el_prof": el, "kern": {}, "copy_gbs": None, "e2e": None, "taps": 3073,
-            "K": 0, "n_out": 0}
+    return {"el": el, "el_prof": el, "el_serial": el, "kern": {}, "copy_gbs": None, "e2e": None,
+            "taps": 3073, "K": 0, "n_out": 0}
 
 
 def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
@@ -570,6 +578,8 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
         el = timed_region(1, batch, world, dist, sync)  # one replay = the K steps
     else:
         el = timed_region(args.steps, run, world, dist, sync)
+    # the same K steps one at a time on one stream (pair 0, D = 1): ms_per_step_serial
+    el_serial = el if D == 1 else timed_region(args.steps, runs[0], world, dist, sync)
     # profiled region: the same K steps with HIP events recorded around every kernel
     # launch on the library's launch stream (per-kernel durations for the roofline;
     # the events add inter-kernel gaps, so this region is not used for `value`).  The
@@ -629,8 +639,8 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
     if args.e2e:
         e2e = e2e_pcie(torch, dev, pfb, ana, syn, n_pol, n_dat, chan_buf, out_buf, args.steps,
                        world, dist)
-    return {"el": el, "el_prof": el_prof, "kern": kern, "copy_gbs": copy_gbs, "e2e": e2e,
-            "taps": len(taps), "K": K, "n_out": n_out}
+    return {"el": el, "el_prof": el_prof, "el_serial": el_serial, "kern": kern, "copy_gbs": copy_gbs,
+            "e2e": e2e, "taps": len(taps), "K": K, "n_out": n_out}
 
 
 def report(args, res, world, workload, n_pol, n_dat, all_seeds):
@@ -667,6 +677,8 @@ def report(args, res, world, workload, n_pol, n_dat, all_seeds):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 4),
+        # the same K steps one at a time on one stream (no step in flight beside another)
+        "ms_per_step_serial": round(res.get("el_serial", el) / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -675,7 +687,10 @@ def report(args, res, world, workload, n_pol, n_dat, all_seeds):
         "config": {"workload": WORKLOAD_NAMES[workload],
                    "n_chan": N_CHAN, "os_factor": OS_STR, "n_taps": res["taps"],
                    "n_dat_per_unit": n_dat, "n_pol_per_gpu": n_pol, "units": world * n_pol,
+                   # every unit the timed region reads: step i runs pair i mod D, whose
+                   # units are the rank's seeds + 7919 (i mod D) (--distinct-inputs)
                    "unit_seeds_per_rank": all_seeds,
+                   "units_in_flight": len(all_seeds[0]) if all_seeds else n_pol,
                    "channelised_rows": res["K"], "output_samples_per_unit": res["n_out"],
                    "parallelism": f"{world} GPU(s) x {n_pol} independent unit(s), one process "
                                   f"per GPU, no collective on the data path",

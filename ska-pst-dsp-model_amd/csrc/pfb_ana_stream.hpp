@@ -1,18 +1,10 @@
 // pfb_ana_stream.hpp — the streaming Bunton analysis for N = 256 (polyphase_analysis.m:83-121),
-// shared by analysis_stream_kernel (pfb_analysis.hip) and the fused round-trip kernel
-// (pfb_roundtrip.hip).
+// analysis_stream_kernel (instantiated in pfb_analysis.hip).
 #pragma once
 #include "pfb_common.hpp"
 
 namespace pfb {
 
-// cache-policy bit of a buffer store/load: sc1 (write-through store / L1-bypassing load) for
-// stage-1 rows handed from one workgroup to another inside a launch
-// (cdna_hip_programming.md Guideline 16, R1)
-constexpr int kSc1 = 16;
-
-// s_waitcnt immediate (gfx9 encoding) waiting for vmcnt <= n only
-constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 
 // Bunton analysis for N = 256 with the FIR in registers and no LDS staging of the
 // input.  View the input as rows of N samples, X[r][c] = x[r N + c].  With M = N DE/NU,
@@ -70,17 +62,9 @@ struct ColMajorLds {
 // ZOUT: 0 no stage-1 rows; 1 rows [row][c] (AnalysisArgs::z); 2 / 4: runs of ZOUT rows per
 // column (AnalysisArgs::zblk) for the synthesis wave kernel.
 // Streaming analysis of step range w of nw (steps of T rows from row0) for polarisation
-// pol.  PUB (fused round trip, pfb_roundtrip.hip): the workgroup publishes its progress —
-// see StepPublisher — after every step; NoPublish otherwise.
-struct NoPublish {
-  static constexpr bool kOn = false;
-  __device__ void step_done(int64_t) const {}
-  __device__ void range_done(int64_t) const {}
-};
-
-template <int N, int P, int NU, int DE, int ZOUT, bool LCBF, bool GS, class PUB>
-__device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int pol, int w, int nw,
-                                                     const PUB& pub) {
+// pol.
+template <int N, int P, int NU, int DE, int ZOUT, bool LCBF, bool GS>
+__device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int pol, int w, int nw) {
   using SH = StreamShape<N, P, NU, DE>;
   constexpr int M = SH::M, PE = SH::PE, QS = SH::QS, T = SH::T, NEW = SH::NEW, WIN = SH::WIN;
   extern __shared__ __attribute__((aligned(16))) float2 smem[];
@@ -89,10 +73,7 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
   const int64_t q_lo = a.row0 / NU;
   const int64_t n_steps = ((a.K + NU - 1) / NU - q_lo + QS - 1) / QS;
   const int64_t st0 = n_steps * w / nw, st1 = n_steps * (w + 1) / nw;
-  if (st0 >= st1) {
-    pub.range_done(0);
-    return;
-  }
+  if (st0 >= st1) return;
 
   // input column c from row DE q_first on; range-checked buffer loads return 0 past n_dat
   const int64_t row_first = (int64_t)DE * (q_lo + st0 * QS);
@@ -155,9 +136,6 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
 #pragma unroll
     for (int i = 0; i < NEW; ++i) pf[i] = ld(rel + WIN + i);
     __syncthreads();  // previous step's FFT has read its rows (first step: F staged)
-    // every wave has passed the previous step's end-of-step wait: the steps before the
-    // previous one have their stage-1 rows in memory
-    if constexpr (PUB::kOn) pub.step_done(stp - st0 - 1);
     // all NU x QS rows accumulate together (tap-outer order): consecutive FMAs are
     // independent, so the 4-cycle FMA latency never stalls issue
     v2f acc[NU][QS];
@@ -207,10 +185,8 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
           constexpr int r1 = qq * NU + s, r0 = r1 - 1;
           constexpr float n2 = (float)N * (float)N;
           const v2f a0 = acc[s - 1][qq] * n2, a1 = acc[s][qq] * n2;
-          // (fused round trip: write-through, the consumer reads them from another CU)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{a0.x, a0.y, a1.x, a1.y}), zb,
-                                                 (uint32_t)((((r0 / ZOUT) * N + c) * ZOUT + r0 % ZOUT) * 8), 0,
-                                                 PUB::kOn ? kSc1 : 0);
+                                                 (uint32_t)((((r0 / ZOUT) * N + c) * ZOUT + r0 % ZOUT) * 8), 0, 0);
         }
       });
     });
@@ -257,23 +233,12 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
     for (int i = 0; i < PE - 1; ++i) win[i] = win[i + NEW];
 #pragma unroll
     for (int i = 0; i < NEW; ++i) win[PE - 1 + i] = pf[i];
-    // fused: at most NEW + T/2 vector-memory operations outstanding.  At least that many
-    // were issued after the previous step's stage-1-row stores (this step's NEW prefetch
-    // loads and T/2 row-pair stores; vmcnt retires in issue order), so those stores are done
-    // — and the wait rarely stalls: it leaves this step's stores and the prefetch in flight
-    if constexpr (PUB::kOn) __builtin_amdgcn_s_waitcnt(waitcnt_vm(NEW + T / 2));
-  }
-  if constexpr (PUB::kOn) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    pub.range_done(st1 - st0);
   }
 }
 
 template <int N, int P, int NU, int DE, int ZOUT, bool LCBF = false, bool GS = false>
 __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
-  analysis_stream_body<N, P, NU, DE, ZOUT, LCBF, GS>(a, blockIdx.y, xcd_tile(blockIdx.x, gridDim.x), gridDim.x,
-                                                      NoPublish{});
+  analysis_stream_body<N, P, NU, DE, ZOUT, LCBF, GS>(a, blockIdx.y, xcd_tile(blockIdx.x, gridDim.x), gridDim.x);
 }
 
 }  // namespace pfb

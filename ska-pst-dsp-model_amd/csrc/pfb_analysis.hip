@@ -646,6 +646,9 @@ static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
                                      : analysis_stream_kernel<N, P, NU, DE, 1>)
               : a.out_rs > 0 ? analysis_stream_kernel<N, P, NU, DE, 0, false, true>
                              : analysis_stream_kernel<N, P, NU, DE, 0>;
+  // the carry (pre) is read only in each workgroup's first WIN-row window prologue: every
+  // pad sample must lie inside the first window (the caller's B <= P N guard)
+  if (a.pre && (a.pad < 0 || a.pad > (int64_t)SH::WIN * N)) return hipErrorInvalidValue;
   hipError_t e = set_lds(kern, SH::lds_bytes);
   if (e != hipSuccess) return e;
   const int64_t q_lo = a.row0 / NU;

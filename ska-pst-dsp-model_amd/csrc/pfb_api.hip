@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -210,6 +211,7 @@ struct PadConsume {
 };
 
 struct pfb_analysis_plan {
+  uint64_t serial = 0;  // unique per plan (the split round trip's key: pointers get reused)
   int device = 0;
   int variant = 0, N = 0, nu = 1, de = 1, M = 0, P = 0, n_pol = 1, sds = 0;
   int C = 0;                  // output channels per row (N; 216 for the LowCBF filterbank)
@@ -404,7 +406,9 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
     return fail(PFB_ERR_NO_DEVICE, "no HIP device available");
   if (d->device < 0 || d->device >= ndev)
     return fail(PFB_ERR_INVALID_ARG, "device %d out of range (%d devices)", d->device, ndev);
+  static std::atomic<uint64_t> next_serial{1};
   auto* p = new pfb_analysis_plan();
+  p->serial = next_serial++;
   p->device = d->device;
   p->variant = d->variant;
   p->N = d->n_chan;
@@ -718,12 +722,17 @@ struct pfb_synthesis_plan {
   DevBuf taper, gainj, sbuf0, sbuf1;  // spectral taper (L), deripple gains (W), scratch
   DevBuf Z, carry, work, stage_in, stage_out;
   int64_t buffered = 0;
-  // one-launch round trip (pfb_roundtrip.hip): progress words, the block schedule of the
-  // last call shape ([9] segment starts, then the blocks), the host-visible timeout word
-  DevBuf rt_prog, rt_sched;
-  int64_t rt_key[5] = {-1, -1, -1, -1, -1};
-  unsigned* rt_err = nullptr;  // pinned, mapped
+  // split round trip: what the analysis half left in Z (analysis plan, n_dat, sample
+  // offset, row layout, rows) — the synthesis half must match it; cleared whenever Z is
+  // written by anything else
+  uint64_t zkey_plan = 0;
+  int64_t zkey[5] = {-1, -1, -1, -1, -1};
 };
+
+static void zkey_clear(pfb_synthesis_plan* p) {
+  p->zkey_plan = 0;
+  std::fill(p->zkey, p->zkey + 5, (int64_t)-1);
+}
 
 static void hann_sym(int L, std::vector<double>& h) {
   h.resize((size_t)L);
@@ -803,6 +812,7 @@ static pfb_status synthesis_chunk(pfb_synthesis_plan* p, const float2* in, int64
     return synthesis_spectral(p, in, in_ps, b0, nb, out, out_ps, out_limit, s);
   }
   const int64_t rows = nb * p->keep + 2 * (int64_t)p->Ov;
+  zkey_clear(p);
   HIPCHK(p->Z.ensure((size_t)p->n_pol * rows * p->N * sizeof(float2)));
   float2* Z = p->Z.as<float2>();
   pfb::ChanIfftArgs c{};
@@ -1134,9 +1144,8 @@ pfb_status pfb_synthesis_plan_destroy(pfb_synthesis_plan* p) {
   (void)hipSetDevice(p->device);
   for (DevBuf* b : {&p->window, &p->tw4, &p->tw4s, &p->twN, &p->twNf, &p->twW, &p->perm, &p->cgain,
                     &p->taper, &p->gainj, &p->sbuf0, &p->sbuf1, &p->Z, &p->carry, &p->work,
-                    &p->stage_in, &p->stage_out, &p->rt_prog, &p->rt_sched})
+                    &p->stage_in, &p->stage_out})
     b->release();
-  if (p->rt_err) (void)hipHostFree(p->rt_err);
   delete p;
   return PFB_OK;
 }
@@ -1323,115 +1332,6 @@ pfb_status pfb_inverse_filterbank_reset(pfb_synthesis_plan* p) {
 // `chan`.  On this chunked path every row and block is computed by the same kernels with
 // the same inputs as pfb_analysis_execute + pfb_synthesis_execute, so both results are
 // bit-identical to the separate calls (the fused path below: see its comment).
-// ------------------------------------------------------------- one-launch round trip
-#ifdef PFB_EXPERIMENTS
-// Synthesis block schedule of the fused kernel (pfb_roundtrip.hip): the analysis runs nA
-// contiguous step ranges (16 rows per step) side by side, ranges [x nA/8, (x+1) nA/8) on XCD
-// x; block b (rows z_row0 + b keep .. + Nf) belongs to the segment of its first range and is
-// ready once every range holding its rows has reached them — at the fraction of the range
-// below.  Each segment's blocks go to that XCD's synthesis workgroups in that order.
-static void round_trip_schedule(int64_t n_steps, int nA, int64_t z_row0, int keep, int Nf, int64_t B,
-                                std::vector<int>& sched) {
-  auto st0 = [&](int64_t w) { return n_steps * w / nA; };
-  auto range_of = [&](int64_t st) { return ((st + 1) * nA + n_steps - 1) / n_steps - 1; };
-  std::vector<std::vector<std::pair<double, int>>> segs(8);
-  for (int64_t b = 0; b < B; ++b) {
-    const int64_t r0 = z_row0 + b * keep;
-    const int64_t s_lo = r0 / 16, s_hi = std::min((r0 + Nf - 1) / 16, n_steps - 1);
-    double ready = 0.0;
-    for (int64_t w = range_of(s_lo); w <= range_of(s_hi); ++w) {
-      const int64_t a0 = st0(w), a1 = st0(w + 1);
-      ready = std::max(ready, (double)(std::min(s_hi + 1, a1) - a0) / (double)std::max<int64_t>(a1 - a0, 1));
-    }
-    const int x = (int)std::min<int64_t>(7, range_of(s_lo) / (nA / 8));
-    segs[(size_t)x].push_back({ready, (int)b});
-  }
-  sched.assign(9, 0);
-  for (int x = 0; x < 8; ++x) {
-    std::sort(segs[(size_t)x].begin(), segs[(size_t)x].end());
-    sched[(size_t)x + 1] = sched[(size_t)x] + (int)segs[(size_t)x].size();
-  }
-  for (int x = 0; x < 8; ++x)
-    for (const auto& e : segs[(size_t)x]) sched.push_back(e.second);
-}
-
-// The fused path as one launch when the shape, the residency (3 workgroups per CU) and
-// the polarisation count allow; *done = false leaves the call to the two-kernel path.
-static pfb_status roundtrip_one_launch(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, const float2* x,
-                                       int64_t in_ps, int64_t n_dat, float2* y, int64_t chan_ps, int64_t K,
-                                       int64_t off, int64_t B, float2* out, int64_t out_ps, int64_t olen,
-                                       hipStream_t s, bool* done) {
-  *done = false;
-  // measured and rejected: experiments build only, PFB_RT_ONE_LAUNCH=1
-  static const bool on = pfb::knob("PFB_RT_ONE_LAUNCH") && std::atoi(pfb::knob("PFB_RT_ONE_LAUNCH")) == 1;
-  if (!on) return PFB_OK;
-  const int cus = pfb::roundtrip_cu_count();
-  const int n_pol = pa->n_pol;
-  if (n_pol != 1 && n_pol != 2 && n_pol != 4) return PFB_OK;
-  const int nA = cus / n_pol, nS = 2 * cus / n_pol;
-  const int groups = ps->N / 16;
-  if (nA <= 0 || nA % 8 != 0 || nS % (8 * groups) != 0) return PFB_OK;
-  const int64_t zrows = (K - off + 15) / 16 * 16;
-  float2* Z = ps->Z.as<float2>();
-  const pfb::AnalysisArgs aa = analysis_args(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, Z, zrows * pa->N, off, 0,
-                                             nullptr, 2);
-  const pfb::SynthBlockArgs sa = synth_args(ps, Z, zrows * pa->N, 0, B, out, out_ps, olen, 2);
-  int per_cu = 0;
-  if (!pfb::roundtrip_fused_supported(aa, sa, &per_cu) || per_cu < 3) return PFB_OK;
-  // analysis steps of the call (launch_stream's count with row0 = 0)
-  const int64_t n_steps = ((K + pa->nu - 1) / pa->nu + (16 / pa->nu) - 1) / (16 / pa->nu);
-  if (n_steps < nA) return PFB_OK;  // every range at least one step
-  // a workgroup's rows must fit one buffer descriptor (launch_stream's rule)
-  if ((n_steps / nA + 2) * 16 * (int64_t)pa->N * 8 + 64 * (int64_t)pa->N * 8 > pfb::kRsrcMaxBytes) return PFB_OK;
-  const int64_t key[5] = {n_steps, nA, off, B, ps->keep};
-  if (!std::equal(key, key + 5, ps->rt_key)) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    HIPCHK(hipStreamIsCapturing(s, &cs));
-    if (cs != hipStreamCaptureStatusNone) return PFB_OK;  // schedule upload is synchronous
-    std::vector<int> sched;
-    round_trip_schedule(n_steps, nA, off, ps->keep, ps->Nf, B, sched);
-    HIPCHK(upload(ps->rt_sched, sched));
-    HIPCHK(ps->rt_prog.ensure((size_t)n_pol * nA * pfb::kProgStride * 4));
-    if (!ps->rt_err) {
-      HIPCHK(hipHostMalloc((void**)&ps->rt_err, 16, hipHostMallocMapped | hipHostMallocCoherent));
-      *ps->rt_err = 0;
-    }
-    std::copy(key, key + 5, ps->rt_key);
-  }
-  if (__atomic_load_n(ps->rt_err, __ATOMIC_ACQUIRE) != 0) {
-    *ps->rt_err = 0;
-    return fail(PFB_ERR_HIP, "an earlier one-launch round trip gave up waiting for its stage-1 rows "
-                             "(workgroups not co-resident): its output is invalid");
-  }
-  unsigned* err_dev = nullptr;
-  HIPCHK(hipHostGetDevicePointer((void**)&err_dev, ps->rt_err, 0));
-  pfb::RtFusedArgs f{};
-  f.prog = ps->rt_prog.as<unsigned>();
-  f.err = err_dev;
-  f.seg = ps->rt_sched.as<int>();
-  f.order = f.seg + 9;
-  f.nA = nA;
-  f.nS = nS;
-  f.lanes = nS / (8 * groups);
-  f.n_steps = n_steps;
-  f.z_row0 = off;
-  static const int nowait = pfb::knob("PFB_RT_NOWAIT") ? std::atoi(pfb::knob("PFB_RT_NOWAIT")) : 0;
-  f.nowait = nowait;
-  static const int prio = pfb::knob("PFB_RT_PRIO") ? std::atoi(pfb::knob("PFB_RT_PRIO")) : 1;
-  f.prio = prio;
-  f.spin_max = 1u << 20;  // >= ~0.1 s per wait: far beyond any real wait
-  HIPCHK(hipMemsetAsync(ps->rt_prog.p, 0, ps->rt_prog.bytes, s));
-  {
-    // algorithmic bytes of the whole round trip (input + channelised product written and
-    // read + output), profiled as one launch
-    const double bytes = (double)n_pol * (8.0 * n_dat + 16.0 * K * pa->N + 8.0 * olen);
-    ProfScope pr(3, bytes, s);
-    HIPCHK(pfb::launch_roundtrip_fused(aa, sa, f, s));
-  }
-  *done = true;
-  return PFB_OK;
-}
-#endif  // PFB_EXPERIMENTS
 
 // phase 0: the whole round trip; 1 / 2: only the analysis / only the synthesis half of the
 // fused path (pfb_roundtrip_analysis_execute / pfb_roundtrip_synthesis_execute), which hand
@@ -1501,10 +1401,17 @@ static pfb_status roundtrip_run(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, c
   const size_t zbytes = (size_t)pa->n_pol * zrows * pa->N * sizeof(float2);
   bool fuse = !no_fuse && analysis_emits_z(pa) && ps->identity_perm && !ps->has_cgain &&
               !ps->has_spectral && ps->chunk_blocks <= 0 && zbytes <= ((size_t)16 << 30);
+  const int64_t zkey[5] = {n_dat, off, zblk, K, zrows};
   if (fuse && phase == 2) {
-    // the synthesis half reads the rows the analysis half left in the plan's scratch
-    if (!ps->Z.p || ps->Z.bytes < zbytes)
-      return fail(PFB_ERR_INVALID_ARG, "split round trip: no stage-1 rows of this size (run the analysis half first)");
+    // the synthesis half reads the rows the analysis half left in the plan's scratch: they
+    // must come from this analysis plan with the same n_dat, offset and row layout
+    if (!ps->Z.p || ps->Z.bytes < zbytes || ps->zkey_plan != pa->serial ||
+        !std::equal(zkey, zkey + 5, ps->zkey))
+      return fail(PFB_ERR_INVALID_ARG,
+                  "split round trip: the synthesis plan holds no stage-1 rows of this analysis plan, "
+                  "n_dat %lld and sample_offset %lld (run pfb_roundtrip_analysis_execute with the same "
+                  "arguments first)",
+                  (long long)n_dat, (long long)sample_offset);
   } else if (fuse) {
     // the rows of the whole call stay resident; a device without room for them takes the
     // chunked pipeline below (its scratch is one chunk's rows) instead of failing
@@ -1521,18 +1428,18 @@ static pfb_status roundtrip_run(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, c
     if (!fuse) return fail(PFB_ERR_UNSUPPORTED, "split round trip: these plans take the chunked pipeline "
                                                 "(use pfb_roundtrip_execute)");
     float2* Z = ps->Z.as<float2>();
-    if (phase == 1)
-      return analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0, nullptr, zblk);
+    if (phase == 1) {
+      zkey_clear(ps);
+      pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0, nullptr,
+                                   zblk);
+      if (st != PFB_OK) return st;
+      ps->zkey_plan = pa->serial;
+      std::copy(zkey, zkey + 5, ps->zkey);
+      return PFB_OK;
+    }
     return synthesis_blocks(ps, Z + (off - z0) * pa->N, zrows * pa->N, 0, B, (float2*)out, out_ps, olen, s, zblk);
   }
-#ifdef PFB_EXPERIMENTS
-  if (fuse && zblk == 2) {
-    bool done = false;
-    pfb_status st = roundtrip_one_launch(pa, ps, x, in_ps, n_dat, y, chan_ps, K, off, B, (float2*)out, out_ps,
-                                         olen, s, &done);
-    if (st != PFB_OK || done) return st;
-  }
-#endif
+  zkey_clear(ps);  // phase 0 reuses Z
   if (fuse) {
     float2* Z = ps->Z.as<float2>();
     static const int conc = pfb::knob("PFB_RT_CONC") ? std::atoi(pfb::knob("PFB_RT_CONC")) : 1;

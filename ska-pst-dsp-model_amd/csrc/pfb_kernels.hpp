@@ -63,7 +63,7 @@ struct AnalysisArgs {
   int64_t pad;
   // with pad > 0: the pad samples in front of `in` are pre[pol][0, pad) (a stream object's
   // carried samples; null: zeros, the LowCBF pre-padding).  Streaming kernel only, read by the
-  // first workgroup's first window (the launcher checks pad <= the window's samples)
+  // first workgroup's first window (launch_stream rejects pad > WIN N; the caller keeps B <= P N)
   const float2* pre;
   int64_t pre_pol_stride;
   float lcbf_scale;  // LowCBF streaming path: output scale (2^12)
@@ -201,28 +201,5 @@ hipError_t launch_synth_wave(const SynthBlockArgs& a, hipStream_t s);
 bool synth_wave512_supported(const SynthBlockArgs& a);
 hipError_t launch_synth_wave512(const SynthBlockArgs& a, hipStream_t s);
 hipError_t launch_synth_block(const SynthBlockArgs& a, hipStream_t s);
-
-// The SKA-Low round trip as one launch (pfb_roundtrip.hip): nA analysis workgroups (step
-// ranges, each publishing its progress) and nS synthesis workgroups (blocks in the order
-// their rows are published) per polarisation.
-constexpr int kProgStride = 16;  // progress words one per 64 B (polls spread over lines)
-struct RtFusedArgs {
-  unsigned* prog;          // [pol][nA][kProgStride] steps of each analysis range in memory
-                           // (word 0 of each slot; zeroed per launch)
-  unsigned* err;           // host-visible word, set when a wait gave up
-  const int* order;        // synthesis blocks of XCD segment x at order[seg[x] .. seg[x+1])
-  const int* seg;          // [9]
-  int nA, nS, lanes;       // per polarisation; lanes = nS / (8 * N / 16) workgroups per phase group and XCD
-  int64_t n_steps;         // analysis steps (16 rows) of the call
-  int64_t z_row0;          // series row of stage-1 row 0
-  unsigned spin_max;       // polls before a wait gives up
-  int nowait;              // experiments build only (PFB_RT_NOWAIT, results invalid): no waits
-  int prio;                // analysis waves at raised issue priority (s_setprio 3)
-};
-// shapes the fused kernel compiles for; *per_cu = its resident workgroups per CU
-bool roundtrip_fused_supported(const AnalysisArgs& aa, const SynthBlockArgs& sa, int* per_cu);
-hipError_t launch_roundtrip_fused(const AnalysisArgs& aa, const SynthBlockArgs& sa, const RtFusedArgs& f,
-                                  hipStream_t s);
-int roundtrip_cu_count();  // compute units of the current device
 
 }  // namespace pfb

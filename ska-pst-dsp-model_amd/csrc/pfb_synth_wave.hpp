@@ -1,6 +1,5 @@
 // pfb_synth_wave.hpp — synthesis stage 2 for Nf = 256 with one output phase per 16 lanes
-// (the algorithm: pfb_synth_wave.hip), shared by synth_wave_kernel and the fused round-trip
-// kernel (pfb_roundtrip.hip).
+// (the algorithm: pfb_synth_wave.hip), instantiated by synth_wave_kernel.
 #pragma once
 #include "pfb_common.hpp"
 
@@ -54,9 +53,9 @@ constexpr int bin_of(int rr) {
 }  // namespace
 
 // The workgroup's blocks: a contiguous range, each block's first 16 - DK register rows
-// taken from the previous block (standalone kernel).  The fused round trip
-// (pfb_roundtrip.hip) supplies its own schedule: blocks in the order their stage-1 rows
-// are published, each waited for before its rows are loaded (sc1 loads).
+// taken from the previous block.  (A schedule class, so that a producer-consumer launch can
+// supply blocks in the order their rows are ready and wait for each — the one-launch
+// round trip measured and rejected in round 3)
 struct RangeSched {
   static constexpr bool kReuse = true;
   static constexpr int kLoadAux = 0;

@@ -18,7 +18,8 @@ from .filterbank import (Channelizer, DeChannelizer, FilterBank, InverseFilterBa
 from .firio import (design_PFB_FIR_filter, design_PFB_FIR_filter_two_stage,
                     read_fir_filter_coeff)
 from .window import PFBWindow, identity_taper
-from .streaming import Impulse, PureTone, TestImpulse, TestPureTone, sgcht
+from .streaming import (FrequencyComb, Impulse, PureTone, TestFrequencyComb, TestImpulse,
+                        TestPureTone, sgcht)
 from . import dada, harness, layout, sharding, verify
 
 __all__ = [
@@ -28,5 +29,6 @@ __all__ = [
     "TwoStageInverseFilterBank", "design_PFB_FIR_filter", "design_PFB_FIR_filter_two_stage",
     "read_fir_filter_coeff", "PFBWindow", "identity_taper", "roundtrip", "roundtrip_analysis",
     "roundtrip_synthesis", "calc_output_nbins",
-    "sgcht", "PureTone", "Impulse", "TestPureTone", "TestImpulse",
+    "sgcht", "PureTone", "Impulse", "FrequencyComb", "TestPureTone", "TestImpulse",
+    "TestFrequencyComb",
 ]

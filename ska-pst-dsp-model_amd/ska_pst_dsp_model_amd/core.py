@@ -46,9 +46,36 @@ def is_device_array(x) -> bool:
     return t is not None and isinstance(x, t.Tensor) and x.is_cuda
 
 
-def _stream_of(x):
+def _stream_of(x, *plans):
+    """The current stream of ``x``'s device as a C handle.  ``plans`` launched on it are
+    marked when the stream is being captured into a graph (``close`` then refuses)."""
     t = _torch()
-    return c_void_p(t.cuda.current_stream(x.device).cuda_stream)
+    s = t.cuda.current_stream(x.device)
+    if plans and t.cuda.is_current_stream_capturing():
+        for p in plans:
+            p._capture_streams.append(s)
+    return c_void_p(s.cuda_stream)
+
+
+def _capturing(plan) -> bool:
+    """Is a stream capture that recorded launches of ``plan`` still active?"""
+    t = _torch()
+    live = []
+    for s in getattr(plan, "_capture_streams", ()):
+        with t.cuda.stream(s):
+            if t.cuda.is_current_stream_capturing():
+                live.append(s)
+    plan._capture_streams = live
+    return bool(live)
+
+
+def _close_guard(plan):
+    # A captured graph references the plan's device buffers (taps, twiddles, stage-1 rows,
+    # carry) by address: freeing them while the capture is open, or before every graph that
+    # replays them is gone, makes the replays read freed memory (INTEGRATION.md §3).
+    if getattr(plan, "_capture_streams", None) and _capturing(plan):
+        raise RuntimeError(f"{type(plan).__name__}.close(): a stream capture that used this plan is "
+                           "still active; end the capture (and drop its graphs) first")
 
 
 def _taps64(filt) -> np.ndarray:
@@ -84,6 +111,7 @@ class AnalysisPlan:
         h = c_void_p()
         _lib.check(lib.pfb_analysis_plan_create(byref(d), byref(h)))
         self._h = h
+        self._capture_streams = []  # streams that captured launches of this plan
         self._lib = lib
         self.out_chan = int(lib.pfb_analysis_output_channels(h))  # 216 for LowCBF
         self.step = (self.n_chan * self.os_factor.de) // self.os_factor.nu
@@ -91,6 +119,7 @@ class AnalysisPlan:
 
     def close(self):
         if getattr(self, "_h", None):
+            _close_guard(self)
             self._lib.pfb_analysis_plan_destroy(self._h)
             self._h = None
 
@@ -131,7 +160,7 @@ class AnalysisPlan:
         _lib.check(self._lib.pfb_filterbank_execute_strided(
             self._h, c_void_p(x.data_ptr()), x.stride(0), n_dat, c_void_p(out.data_ptr()),
             int(out_pol_stride), int(row_stride), int(chan_stride), int(sel[0]), int(sel[1]),
-            int(sel[2]), int(cap), byref(n_out), _stream_of(x)))
+            int(sel[2]), int(cap), byref(n_out), _stream_of(x, self)))
         return int(n_out.value)
 
     def _prep_in(self, x):
@@ -174,7 +203,7 @@ class AnalysisPlan:
         n_out = c_int64(0)
         if dev:
             src, dst, mem, stream = c_void_p(x.data_ptr()), c_void_p(out.data_ptr()), \
-                _lib.PFB_MEM_DEVICE, _stream_of(x)
+                _lib.PFB_MEM_DEVICE, _stream_of(x, self)
         else:
             src, dst, mem, stream = x.ctypes.data_as(c_void_p), out.ctypes.data_as(c_void_p), \
                 _lib.PFB_MEM_HOST, c_void_p(0)
@@ -266,6 +295,7 @@ class SynthesisPlan:
         h = c_void_p()
         _lib.check(lib.pfb_synthesis_plan_create(byref(d), byref(h)))
         self._h = h
+        self._capture_streams = []  # streams that captured launches of this plan
         self._lib = lib
         W = (nf * self.os_factor.de) // self.os_factor.nu
         self.output_fft_length = W * self.n_chan
@@ -275,6 +305,7 @@ class SynthesisPlan:
 
     def close(self):
         if getattr(self, "_h", None):
+            _close_guard(self)
             self._lib.pfb_synthesis_plan_destroy(self._h)
             self._h = None
 
@@ -326,7 +357,7 @@ class SynthesisPlan:
             t = _torch()
             out = t.empty((self.n_pol, max(cap, 0)), dtype=t.complex64, device=ptc.device)
             src, dst, mem, stream = c_void_p(ptc.data_ptr()), c_void_p(out.data_ptr()), \
-                _lib.PFB_MEM_DEVICE, _stream_of(ptc)
+                _lib.PFB_MEM_DEVICE, _stream_of(ptc, self)
         else:
             out = np.empty((self.n_pol, max(cap, 0)), dtype=np.complex64)
             src, dst, mem, stream = ptc.ctypes.data_as(c_void_p), out.ctypes.data_as(c_void_p), \
@@ -374,7 +405,7 @@ def roundtrip(analysis: AnalysisPlan, synthesis: SynthesisPlan, x, sample_offset
     _lib.check(_lib.load().pfb_roundtrip_execute(
         analysis._h, synthesis._h, c_void_p(x.data_ptr()), n_dat, n_dat,
         c_void_p(chan.data_ptr()), K * analysis.n_chan, K, byref(kr), int(sample_offset),
-        c_void_p(out.data_ptr()), max(n_out, 1), n_out, byref(no), _stream_of(x)))
+        c_void_p(out.data_ptr()), max(n_out, 1), n_out, byref(no), _stream_of(x, analysis, synthesis)))
     return chan, out
 
 
@@ -401,7 +432,8 @@ def roundtrip_analysis(analysis: AnalysisPlan, synthesis: SynthesisPlan, x, samp
     kr = c_int64(0)
     _lib.check(_lib.load().pfb_roundtrip_analysis_execute(
         analysis._h, synthesis._h, c_void_p(x.data_ptr()), n_dat, n_dat,
-        c_void_p(chan.data_ptr()), K * analysis.n_chan, K, byref(kr), int(sample_offset), _stream_of(x)))
+        c_void_p(chan.data_ptr()), K * analysis.n_chan, K, byref(kr), int(sample_offset),
+        _stream_of(x, analysis, synthesis)))
     return chan
 
 
@@ -423,7 +455,7 @@ def roundtrip_synthesis(analysis: AnalysisPlan, synthesis: SynthesisPlan, n_dat:
     no = c_int64(0)
     _lib.check(_lib.load().pfb_roundtrip_synthesis_execute(
         analysis._h, synthesis._h, int(n_dat), int(sample_offset), c_void_p(out.data_ptr()),
-        max(n_out, 1), n_out, byref(no), _stream_of(out)))
+        max(n_out, 1), n_out, byref(no), _stream_of(out, analysis, synthesis)))
     return out
 
 

@@ -33,8 +33,8 @@ import numpy as np
 from .config import as_rational, config_dir, default_config
 from .firio import design_PFB_FIR_filter, design_PFB_FIR_filter_two_stage, read_fir_filter_coeff
 
-__all__ = ["PureTone", "Impulse", "TestPureTone", "TestImpulse", "sgcht", "sgcht_config",
-           "header_template"]
+__all__ = ["PureTone", "Impulse", "FrequencyComb", "TestPureTone", "TestImpulse",
+           "TestFrequencyComb", "comb_harmonics", "sgcht", "sgcht_config", "header_template"]
 
 
 # ------------------------------------------------------------------ generators
@@ -79,6 +79,48 @@ class Impulse:
             x[0] = 0.0
         self.current += nsample
         return self, x[None, None, :]
+
+
+class FrequencyComb:
+    """FrequencyComb.m:1-40: one PureTone per harmonic (amplitude, frequency), each
+    carrying its own phase across calls; the block is the single-precision sum of the
+    tones' single-precision blocks, accumulated in harmonic order as the Matlab loop
+    does (``x = x + tmp``)."""
+
+    def __init__(self, amplitudes, frequencies):
+        self.tone = [PureTone(frequency=float(f), amplitude=float(a))
+                     for a, f in zip(np.ravel(amplitudes), np.ravel(frequencies))]
+        self.ntone = len(self.tone)
+
+    def generate(self, nsample: int):
+        x = np.zeros(nsample, dtype=np.complex64)
+        for tone in self.tone:
+            _, tmp = tone.generate(nsample)
+            x = x + tmp[0, 0]
+        return self, x[None, None, :]
+
+
+def comb_harmonics(n_chan=1, two_stage=False, invert=False, comb="", nharmonic=32):
+    """sgcht.m:394-431: (amplitudes, frequencies) of the frequency-comb test signal —
+    linspace(1, sqrt 2) amplitudes; frequencies from -0.5 + 1/(4 nharmonic) in steps of
+    1/nharmonic, scaled into one coarse or fine channel for ``comb`` 'coarse' / 'fine',
+    otherwise moved a quarter channel of the output channels (n_chan, n_chan^2 two-stage,
+    one stage fewer when inverting) off the DC bins."""
+    amplitudes = np.linspace(1.0, math.sqrt(2.0), nharmonic)
+    fmin = -0.5 + 1.0 / (nharmonic * 4)
+    fmax = fmin + (nharmonic - 1.0) / nharmonic
+    if comb == "coarse":
+        fmin, fmax = fmin / n_chan, fmax / n_chan
+    elif comb == "fine":
+        fmin, fmax = fmin / n_chan ** 2, fmax / n_chan ** 2
+    elif n_chan > 1:
+        nch = n_chan ** 2 if two_stage else n_chan
+        if invert:
+            nch = nch / n_chan
+        if nch > 1:
+            fmin += 1.0 / (nch * 4)
+            fmax += 1.0 / (nch * 4)
+    return amplitudes, np.linspace(fmin, fmax, nharmonic)
 
 
 # ------------------------------------------------------------------ testers
@@ -157,13 +199,65 @@ class TestImpulse:
                     w = float(amp_dB[outside].max())
                     worst = max(worst, w)
                     if w > self.dB_max:
-                        # (the position advances even on a failure: sgcht.m stops at the
-                        # first one, a caller scoring every block does not)
-                        self.current += nsample
+                        # TestImpulse.m:67-70 returns without advancing obj.current
                         self.last = {"fail": "outside", "dB": w, "off": off}
                         return self, -1
         self.current += nsample
         self.last = {"max_outside_dB": worst, "off": off}
+        return self, 0
+
+
+class TestFrequencyComb:
+    """TestFrequencyComb.m:15-118 — per polarisation and channel: nfft = block length (at
+    most 8 Ki), |FFT(x)| / (nfft nchan); every harmonic that falls in this channel
+    (jchan = floor(f nchan) mod nchan) must reach >= 0.5 at bin
+    floor((f - ichan/nchan) hfac) mod nfft, where hfac = nchan nfft normalised by the
+    oversampling factor once per analysis level left in the data (level = 2 two-stage, 1
+    one stage with nchan > 1, minus one each for invert and critical).
+
+    Each harmonic is checked in the one channel it falls in (the Matlab double loop over
+    channels and harmonics visits exactly those pairs), so the verdict is the same."""
+
+    __test__ = False
+
+    def __init__(self, frequencies=(), os_factor="1/1", two_stage=False, invert=False,
+                 critical=False):
+        self.frequencies = np.ravel(np.asarray(frequencies, dtype=np.float64))
+        self.os_factor = as_rational(os_factor)
+        self.two_stage = two_stage
+        self.invert = invert
+        self.critical = critical
+        self.last = None
+
+    def test(self, x):
+        x = _host(x)
+        npol, nchan, n = x.shape
+        nfft = min(n, 8 * 1024)
+        if nfft == 0:
+            self.last = {"min_level": None}
+            return self, 0
+        level = 2 if self.two_stage else (1 if nchan > 1 else 0)
+        level -= int(bool(self.invert)) + int(bool(self.critical))
+        hfac = nchan * nfft
+        for _ in range(max(level, 0)):
+            hfac = (self.os_factor.de * hfac) / self.os_factor.nu  # normalize.m
+        f = self.frequencies
+        jchan = np.mod(np.floor(f * nchan).astype(np.int64) + nchan, nchan)
+        iharm = np.mod(np.floor((f - jchan / nchan) * hfac).astype(np.int64) + nfft, nfft)
+        worst = np.inf
+        for ipol in range(npol):
+            spec = np.abs(np.fft.fft(x[ipol, jchan, :nfft].astype(np.complex128), axis=-1)
+                          / (nfft * nchan))
+            lv = spec[np.arange(f.size), iharm]
+            worst = min(worst, float(lv.min()))
+            bad = np.nonzero(lv < 0.5)[0]
+            if bad.size:
+                i = int(bad[0])
+                self.last = {"fail": "harmonic", "harmonic": i, "frequency": float(f[i]),
+                             "chan": int(jchan[i]), "bin": int(iharm[i]), "level": float(lv[i]),
+                             "nfft": nfft}
+                return self, -1
+        self.last = {"min_level": worst, "nfft": nfft}
         return self, 0
 
 
@@ -194,17 +288,27 @@ def sgcht_config(cfg: str):
 
 def sgcht(signal="complex_sinusoid", cfg="", two_stage=False, invert=False, critical=False,
           combine=1, test=True, blocks=None, blocksz=None, device=0, collect=False,
-          noise=1e-6, seed=0):
+          noise=1e-6, seed=0, comb=""):
     """sgcht.m with ``test=true``: returns a namespace with ``result`` (0 pass, -1 fail, as
     sgcht returns), ``blocks`` (blocks processed), ``tester`` (the tester object, its
     ``last`` diagnostics), ``config`` and, with ``collect``, ``outputs`` (the blocks the
     tester saw, device tensors) and ``inputs`` (the generated host blocks).
 
+    Signals: complex_sinusoid (TestPureTone), temporal_impulse (TestImpulse) and
+    frequency_comb (TestFrequencyComb; ``comb`` '', 'coarse' or 'fine', sgcht.m:394-432).
+    sgcht.m:439 assigns ``tester.os_factor = os_factor``, a name sgcht never defines (Matlab
+    would stop there for any comb test with a cfg); the configuration's os_factor — the
+    evident intent — is used.
+
     Block size / count default to sgcht.m:480-495 (64 Ki samples x 2048 blocks single
-    stage, 64 Mi x 2 two-stage, doubled for 'mid'); tests pass smaller counts."""
-    if signal not in ("complex_sinusoid", "temporal_impulse"):
-        raise ValueError(f"sgcht: testing is implemented for complex_sinusoid and "
-                         f"temporal_impulse, not {signal!r}")
+    stage, 128 blocks for the comb, 64 Mi x 2 two-stage, doubled for 'mid'); tests pass
+    smaller counts."""
+    if signal not in ("complex_sinusoid", "temporal_impulse", "frequency_comb"):
+        raise ValueError(f"sgcht: testing is implemented for complex_sinusoid, "
+                         f"temporal_impulse and frequency_comb, not {signal!r}")
+    if comb and (not cfg or signal != "frequency_comb"):  # sgcht.m:106-114
+        raise ValueError("Cannot specify comb spacing without analysis filterbank cfg "
+                         "and a frequency_comb signal")
     from .filterbank import (FilterBank, InverseFilterBank, TwoStageFilterBank,
                              TwoStageInverseFilterBank)
     if two_stage and not cfg:
@@ -243,8 +347,14 @@ def sgcht(signal="complex_sinusoid", cfg="", two_stage=False, invert=False, crit
         if cfg == "mid":
             blocksz *= 2
     if blocks is None:
-        blocks = 2 if two_stage else 2 * 1024
-    if signal == "complex_sinusoid":
+        blocks = 2 if two_stage else (128 if signal == "frequency_comb" else 2 * 1024)
+    if signal == "frequency_comb":
+        amps, freqs = comb_harmonics(n_chan, two_stage, invert, comb)
+        gen = FrequencyComb(amps, freqs)
+        tester = TestFrequencyComb(freqs)
+        if config is not None:
+            tester = TestFrequencyComb(freqs, config.os_factor, two_stage, invert, critical)
+    elif signal == "complex_sinusoid":
         gen = PureTone(frequency=float(header["TONEFREQ"]) * tsamp / 1e6)  # sgcht.m:423-426
         tester = TestPureTone(frequency=gen.frequency)
     else:

@@ -61,7 +61,10 @@ def test_gpus_2_launches_two_ranks_and_aggregates():
     cfg = d["config"]
     assert cfg["workload"].startswith("C4")
     assert cfg["n_pol_per_gpu"] == 2 and cfg["units"] == 4
-    assert cfg["unit_seeds_per_rank"] == [[100, 101], [102, 103]]
+    # 3 steps in flight (default), each plan pair on its own units (seeds + 7919 p)
+    assert cfg["unit_seeds_per_rank"] == [[100, 101, 8019, 8020, 15938, 15939],
+                                          [102, 103, 8021, 8022, 15940, 15941]]
+    assert cfg["units_in_flight"] == 6
     # value = all ranks' samples / max-over-ranks time
     samples = 2 * 2 * cfg["n_dat_per_unit"] * steps
     t = d["ms_per_step"] * steps / 1e3
@@ -75,7 +78,13 @@ def test_gpus_1_is_the_c2_headline():
     d = _json_line(r.stdout)
     assert d["n_gpus"] == 1
     assert d["config"]["workload"].startswith("C2")
-    assert d["config"]["unit_seeds_per_rank"] == [[100]]
+    assert d["config"]["unit_seeds_per_rank"] == [[100, 8019, 15938]]
+    assert d["config"]["units_in_flight"] == 3
+    assert d["ms_per_step_serial"] > 0
+    r = _run(["--stub-device", "--steps", "2", "--warmup", "0", "--no-cpu-baseline",
+              "--inflight", "1"])
+    d = _json_line(r.stdout)
+    assert d["config"]["unit_seeds_per_rank"] == [[100]] and d["config"]["units_in_flight"] == 1
 
 
 def test_gpus_must_match_launcher_world():
@@ -104,8 +113,8 @@ def test_env_is_recorded():
 def _report(workload, kernels, n_pol):
     class A:
         steps, warmup, graph, roundtrip, stub_device = 10, 3, 1, 1, True
-    res = {"el": 1e-3, "el_prof": 1e-3, "kern": kernels, "copy_gbs": None, "e2e": None,
-           "taps": 3073, "K": 74883, "n_out": 16737280}
+    res = {"el": 1e-3, "el_prof": 1e-3, "el_serial": 1.5e-3, "kern": kernels, "copy_gbs": None,
+           "e2e": None, "taps": 3073, "K": 74883, "n_out": 16737280}
     return bench.report(A, res, 1, workload, n_pol, 1 << 24, [[100]])
 
 
@@ -126,3 +135,21 @@ def test_roofline_traffic_is_the_pmc_record_of_the_timed_kernel():
     kern["analysis+chan_ifft"]["kernel"] = "void pfb::not_profiled<2>(pfb::AnalysisArgs)"
     roof = _report("c2", kern, 1)["roofline"]
     assert roof["traffic"] is None and "not_profiled<2>" in roof["traffic_missing"]
+
+
+def test_report_states_what_was_timed():
+    """The line lists every unit seed the timed region reads, the units in flight, and the
+    one-at-a-time step time beside the pipelined one."""
+    out = _report("c2", {}, 1)
+    assert out["ms_per_step"] == 0.1 and out["ms_per_step_serial"] == 0.15
+    seeds = bench.pair_seeds([100], 3, True)
+    assert seeds == [100, 8019, 15938]
+    assert bench.pair_seeds([100, 101], 2, False) == [100, 101, 100, 101]
+    class A:
+        steps, warmup, graph, roundtrip, stub_device, inflight = 10, 3, 1, 1, True, 3
+    res = {"el": 1e-3, "el_prof": 1e-3, "el_serial": 1.7e-3, "kern": {}, "copy_gbs": None,
+           "e2e": None, "taps": 3073, "K": 74883, "n_out": 16737280}
+    out = bench.report(A, res, 1, "c2", 1, 1 << 24, [seeds])
+    assert out["config"]["unit_seeds_per_rank"] == [[100, 8019, 15938]]
+    assert out["config"]["units_in_flight"] == 3
+    assert out["ms_per_step_serial"] == 0.17

@@ -197,3 +197,71 @@ def test_sgcht_without_channelizer_passes():
     assert sgcht.sgcht(signal="complex_sinusoid", blocks=3, blocksz=4096).result == 0
     r = sgcht.sgcht(signal="temporal_impulse", blocks=3, blocksz=16384)
     assert r.result == 0 and r.tester.current == 3 * 16384
+
+
+def test_test_impulse_does_not_advance_on_failure():
+    """TestImpulse.m:67-70 returns -1 without advancing obj.current."""
+    from ska_pst_dsp_model_amd import streaming as sgcht
+    x = np.zeros((1, 1, 100), np.complex64)
+    x[0, 0, 70] = 1.0
+    t = sgcht.TestImpulse(offset=10)
+    assert t.test(x)[1] == -1 and t.current == 0
+
+
+def test_frequency_comb_generator_and_harmonics():
+    """FrequencyComb.m: the single-precision sum of its PureTones, phase carried across
+    calls; sgcht.m:394-431's harmonic grid with the quarter-channel offsets."""
+    from ska_pst_dsp_model_amd import streaming as sgcht
+    amps, f = sgcht.comb_harmonics()
+    assert f.size == 32 and np.isclose(f[0], -0.5 + 1 / 128) and np.isclose(f[1] - f[0], 1 / 32)
+    assert np.isclose(amps[0], 1.0) and np.isclose(amps[-1], np.sqrt(2))
+    _, f1 = sgcht.comb_harmonics(256)
+    assert np.isclose(f1[0] - f[0], 1 / 1024)
+    _, f2 = sgcht.comb_harmonics(256, two_stage=True, invert=True)
+    assert np.allclose(f2, f1)
+    _, fc = sgcht.comb_harmonics(256, comb="coarse")
+    assert np.allclose(fc, f / 256)
+    g = sgcht.FrequencyComb(amps, f)
+    _, a = g.generate(100)
+    _, b = g.generate(60)
+    whole = sgcht.FrequencyComb(amps, f).generate(160)[1]
+    assert np.array_equal(np.concatenate([a, b], axis=2), whole)
+    ref = np.zeros(160, np.complex64)
+    for ai, fi in zip(amps, f):
+        ref = ref + (ai * np.exp(2j * np.pi * fi * np.arange(160))).astype(np.complex64)
+    assert np.array_equal(whole[0, 0], ref)
+
+
+def test_frequency_comb_tester_equals_literal_loop():
+    """TestFrequencyComb (one FFT per harmonic's channel) gives the verdict of the literal
+    channel x harmonic loop of TestFrequencyComb.m:15-118 (verify.frequency_comb_test) on
+    the comb itself (level 0, passing and failing) and on oracle channelised combs
+    (level 1)."""
+    from ska_pst_dsp_model_amd import streaming as sgcht
+    from ska_pst_dsp_model_amd import verify
+    from ska_pst_dsp_model_amd.firio import design_PFB_FIR_filter
+    from oracle import pfb_oracle as orc
+    amps, f = sgcht.comb_harmonics()
+    x = sgcht.FrequencyComb(amps, f).generate(8192)[1]
+    t = sgcht.TestFrequencyComb(f)
+    assert t.test(x)[1] == 0 == verify.frequency_comb_test(x, f)
+    # drop one harmonic: both fail
+    x_bad = sgcht.FrequencyComb(amps[1:], f[1:]).generate(8192)[1]
+    assert t.test(x_bad)[1] == -1 == verify.frequency_comb_test(x_bad, f)
+    taps = design_PFB_FIR_filter(16, "8/7", 10)
+    amps, f = sgcht.comb_harmonics(16)
+    xc = sgcht.FrequencyComb(amps, f).generate(16 * 14 * 600)[1]
+    ch = orc.polyphase_analysis(xc, taps, 16, "8/7")
+    for scale in (1.0, 1e-3):
+        got = sgcht.TestFrequencyComb(f, "8/7").test(scale * ch)[1]
+        assert got == verify.frequency_comb_test(scale * ch, f, "8/7")
+    # (channel k of the Bunton bank is centred on k/N while the tester assigns harmonic f to
+    # channel floor(f N): the harmonics at k + 7/8 lie outside their channel's passband, so
+    # the channelised comb fails TestFrequencyComb in the reference's own rules too)
+    assert sgcht.TestFrequencyComb(f, "8/7").test(ch)[1] == -1
+
+
+def test_sgcht_frequency_comb_without_channelizer_passes():
+    from ska_pst_dsp_model_amd import streaming as sgcht
+    r = sgcht.sgcht(signal="frequency_comb", blocks=3, blocksz=8192)
+    assert r.result == 0 and r.blocks == 3

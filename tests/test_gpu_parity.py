@@ -403,6 +403,39 @@ def test_filterbank_stream_carry_in_place(gpu, os_, tpc):
     assert torch.equal(streamed, whole[:, :, :streamed.shape[2]])
 
 
+def test_filterbank_stream_padded(gpu):
+    """Streaming FilterBank on the SKA-Mid padded (commutator) analysis: 4096 channels,
+    100 353 two-stage taps, 8/7 (FilterBank.m:85-126 calling polyphase_analysis_padded).
+    The Matlab object calls the padded analysis on carry + chunk every time, so each call
+    restarts the commutator with zero history (polyphase_analysis_padded.m:101-102) and
+    circularly shifts its own rows by -sds (:156) — the reference defect SURVEY §8(c)
+    names; the engine reproduces it by running the analysis over the concatenated call
+    input (pfb_filterbank_execute: all K rows, the nu-trimmed Kt copied out).  Chunks are
+    shorter than M (3584: no output row, everything carried), shorter and longer than
+    P N (102 400), and two polarisations; every chunk is compared with the oracle object
+    and the carry lengths must match."""
+    import torch
+    pfb = _pfb()
+    taps = _taps("mid")
+    cfg = dict(analysis_function="polyphase_analysis_padded", filt_coeff=taps, channels=4096,
+               os_factor="8/7")
+    fb = pfb.FilterBank(cfg)
+    ofb = orc.FilterBankOracle(taps, 4096, "8/7", "polyphase_analysis_padded")
+    rng = np.random.default_rng(47)
+    chunks = (3000, 131072, 50000, 2000, 262144, 100000, 1 << 17)
+    for i, n in enumerate(chunks):
+        x = _noise(rng, (2, 1, n))
+        xd = torch.from_numpy(x).to(gpu) if i % 2 else x  # device and host inputs
+        fb, got = fb.execute(xd)
+        ref = ofb.execute(x)
+        got = got.cpu().numpy() if hasattr(got, "cpu") else np.asarray(got)
+        assert got.shape == ref.shape, (n, got.shape, ref.shape)
+        if ref.size:
+            assert_pfb_close(got, ref, what=f"padded stream chunk {i} ({n} samples)")
+        assert fb.buffered_samples == ofb.buffered_samples, (n, fb.buffered_samples,
+                                                             ofb.buffered_samples)
+
+
 def test_inverse_filterbank_streaming_matches_oracle(gpu):
     pfb = _pfb()
     taps = _taps("test")

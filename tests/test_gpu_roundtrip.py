@@ -200,7 +200,9 @@ def test_roundtrip_steps_in_flight(gpu):
     (256, 256, 48, "polyphase_analysis"),           # streaming analysis + wave synthesis
     (512, 512, 128, "polyphase_analysis_padded"),   # register-window FIR + row FFT + wave512
 ])
-def test_roundtrip_split_halves(gpu, N, nf, ov, variant):
+@pytest.mark.parametrize("so", [1, 17, 162])        # off 0 / 16: run layout; 161: row layout
+@pytest.mark.parametrize("n_pol", [1, 2])
+def test_roundtrip_split_halves(gpu, N, nf, ov, variant, so, n_pol):
     """pfb_roundtrip_analysis_execute + pfb_roundtrip_synthesis_execute (the halves bench.py
     pipelines over two streams) equal pfb_roundtrip_execute bit for bit — also when the
     halves run on two streams ordered by an event; the synthesis half of a fresh plan (no
@@ -208,31 +210,101 @@ def test_roundtrip_split_halves(gpu, N, nf, ov, variant):
     import torch
     pfb = _pfb()
     taps = pfb.design_PFB_FIR_filter(N, "8/7", 12)
-    x = _noise_t(torch, gpu, (2, 1 << 20), 17)
+    x = _noise_t(torch, gpu, (n_pol, 1 << 20), 17)
     win = pfb.PFBWindow().lookup["tukey"](nf, ov)
 
     def plans():
-        return (pfb.AnalysisPlan(taps, N, "8/7", variant, 2, 0),
-                pfb.SynthesisPlan(N, "8/7", nf, ov, True, 1, True, taps, win, None, 2, 0))
+        return (pfb.AnalysisPlan(taps, N, "8/7", variant, n_pol, 0),
+                pfb.SynthesisPlan(N, "8/7", nf, ov, True, 1, True, taps, win, None, n_pol, 0))
     ana, syn = plans()
-    c_ref, o_ref = pfb.roundtrip(ana, syn, x, sample_offset=1)
+    c_ref, o_ref = pfb.roundtrip(ana, syn, x, sample_offset=so)
     c_ref, o_ref = c_ref.clone(), o_ref.clone()
     ana2, syn2 = plans()
     with pytest.raises(pfb.PfbError):
-        pfb.roundtrip_synthesis(ana2, syn2, x.shape[1], device=gpu.index or 0)
-    chan = pfb.roundtrip_analysis(ana2, syn2, x)
+        pfb.roundtrip_synthesis(ana2, syn2, x.shape[1], sample_offset=so, device=gpu.index or 0)
+    chan = pfb.roundtrip_analysis(ana2, syn2, x, sample_offset=so)
     sa, ss = torch.cuda.current_stream(), torch.cuda.Stream()
     ev = torch.cuda.Event()
     ev.record(sa)
     ss.wait_event(ev)
     with torch.cuda.stream(ss):
-        out = pfb.roundtrip_synthesis(ana2, syn2, x.shape[1], device=gpu.index or 0)
+        out = pfb.roundtrip_synthesis(ana2, syn2, x.shape[1], sample_offset=so, device=gpu.index or 0)
     torch.cuda.synchronize()
     assert torch.equal(chan, c_ref)
     assert torch.equal(out, o_ref)
     syn2.set_chunk_blocks(2)
     with pytest.raises(pfb.PfbError):
-        pfb.roundtrip_analysis(ana2, syn2, x)
+        pfb.roundtrip_analysis(ana2, syn2, x, sample_offset=so)
+
+
+@pytest.mark.parametrize("N,nf,ov,variant", [
+    (256, 256, 48, "polyphase_analysis"),
+    (512, 512, 128, "polyphase_analysis_padded"),
+])
+def test_roundtrip_split_halves_reject_mismatch(gpu, N, nf, ov, variant):
+    """The synthesis half checks that the stage-1 rows in its scratch came from the analysis
+    half of THIS analysis plan with the same n_dat and sample_offset: another
+    n_dat, another offset, another analysis plan, or rows overwritten by a whole round trip
+    on the pair are rejected with PfbError instead of synthesising stale rows."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(N, "8/7", 12)
+    x = _noise_t(torch, gpu, (1, 1 << 19), 23)
+    win = pfb.PFBWindow().lookup["tukey"](nf, ov)
+    ana = pfb.AnalysisPlan(taps, N, "8/7", variant, 1, 0)
+    ana_b = pfb.AnalysisPlan(taps, N, "8/7", variant, 1, 0)
+    syn = pfb.SynthesisPlan(N, "8/7", nf, ov, True, 1, True, taps, win, None, 1, 0)
+    dev = gpu.index or 0
+    pfb.roundtrip_analysis(ana, syn, x, sample_offset=17)
+    for kw in (dict(n_dat=x.shape[1] - 4096, sample_offset=17), dict(n_dat=x.shape[1], sample_offset=1)):
+        with pytest.raises(pfb.PfbError):
+            pfb.roundtrip_synthesis(ana, syn, kw["n_dat"], sample_offset=kw["sample_offset"], device=dev)
+    with pytest.raises(pfb.PfbError):
+        pfb.roundtrip_synthesis(ana_b, syn, x.shape[1], sample_offset=17, device=dev)
+    # the matching call still works after the rejected ones
+    out = pfb.roundtrip_synthesis(ana, syn, x.shape[1], sample_offset=17, device=dev)
+    _, o_ref = pfb.roundtrip(ana_b, syn, x, sample_offset=17)
+    torch.cuda.synchronize()
+    assert torch.equal(out, o_ref)
+    # the whole round trip just reused the pair's rows: the synthesis half alone is refused
+    with pytest.raises(pfb.PfbError):
+        pfb.roundtrip_synthesis(ana_b, syn, x.shape[1], sample_offset=17, device=dev)
+
+
+def test_plan_close_refused_during_capture(gpu):
+    """A plan whose launches a stream capture recorded cannot be closed while that capture
+    is open (its device buffers are referenced by the graph: the round-3 use-after-free);
+    after the capture ends and the graph is replayed and dropped, close() works."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
+    win = pfb.PFBWindow().lookup["tukey"](256, 48)
+    x = _noise_t(torch, gpu, (1, 1 << 18), 29)
+    ana = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
+    syn = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, 1, 0)
+    chan, out = pfb.roundtrip(ana, syn, x)  # warm-up: allocates the plan scratch
+    ref = out.clone()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g.capture_begin()
+        try:
+            pfb.roundtrip(ana, syn, x, chan=chan, out=out)
+            with pytest.raises(RuntimeError):
+                ana.close()
+            with pytest.raises(RuntimeError):
+                syn.close()
+        finally:
+            g.capture_end()
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    del g
+    ana.close()
+    syn.close()
 
 
 # ------------------------------------------------------------------ BASELINE C2 size
