@@ -70,9 +70,13 @@ def _run_chain(pfb, signal, cfg_name, two_stage=False, invert=False, critical=Fa
             # 4096-channel SKA-Mid bank — a tone's bins and the stopband leakage of 65 536
             # fine / 4096 / 256 coarse channels span many decades, and a tone in 1-2 of
             # 4096 channels has an RMS ~50x below its peak)
+            # (the 32-harmonic comb is not unit amplitude — |x| reaches ~38 — so its
+            # inverted series is brought to unit amplitude by its RMS, ~6.9, first)
             tone_mid = signal != "temporal_impulse" and res.n_chan >= 4096
-            scale = 1.0 if (invert and not two_stage) else (
-                "peak" if (two_stage or tone_mid) else "rms")
+            if invert and not two_stage:
+                scale = "rms" if signal == "frequency_comb" else 1.0
+            else:
+                scale = "peak" if (two_stage or tone_mid) else "rms"
             assert_pfb_close(got, ref, scale=scale,
                              what=f"sgcht {cfg_name} {signal} 2stg={two_stage} inv={invert} "
                                   f"crit={critical} comb={combine} block {i}")
