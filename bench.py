@@ -92,6 +92,10 @@ def parse():
                          "(seeds + 7919 p), so overlapping steps share no input data")
     ap.add_argument("--kernel-events", type=int, default=1,
                     help="record HIP events around every kernel in the timed region")
+    ap.add_argument("--stage1", choices=("auto", "stored", "recomputed"), default="auto",
+                    help="synthesis stage-1 rows of the fused round trip "
+                         "(pfb_synthesis_set_stage1_rows): written by the analysis and read back, "
+                         "or recomputed from the input by the synthesis (bit-identical output)")
     ap.add_argument("--e2e", type=int, default=0,
                     help="also time the host-buffer path: pinned DADA bytes (NBIT 8 TFP) -> "
                          "H2D -> unpack -> round trip -> pack (NBIT 32) -> D2H (reported as "
@@ -481,6 +485,7 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
         syn = pfb.SynthesisPlan(N_CHAN, OS_STR, NF, OV, True, 1, True, taps, win, None, n_pol, local)
         if args.chunk_blocks:
             syn.set_chunk_blocks(args.chunk_blocks)
+        syn.set_stage1_rows(args.stage1)
         K = ana.output_length(n_dat)
         n_out = syn.output_length(K)
         chan_buf = torch.empty((n_pol, K, N_CHAN), dtype=torch.complex64, device=dev)
@@ -698,7 +703,8 @@ def report(args, res, world, workload, n_pol, n_dat, all_seeds):
                    "steps_in_flight": max(1, getattr(args, "inflight", 1)),
                    "pipeline": bool(getattr(args, "pipeline", 0)) and max(1, getattr(args, "inflight", 1)) > 1,
                    "distinct_inputs_per_pair": bool(getattr(args, "distinct_inputs", 1)),
-                   "roundtrip_call": bool(args.roundtrip)},
+                   "roundtrip_call": bool(args.roundtrip),
+                   "stage1_rows": getattr(args, "stage1", "auto")},
         "roofline": roof,
         "round_trip_hbm_frac": round(rt_gbs / HBM_PEAK_GBS, 4),
         "ms_per_step_with_kernel_events": round(res["el_prof"] / args.steps * 1e3, 4),

@@ -195,6 +195,22 @@ pfb_status pfb_inverse_filterbank_reset(pfb_synthesis_plan* plan);
 /* Blocks processed per channel-IFFT/block-kernel chunk (scratch = chunk * keep rows). */
 pfb_status pfb_synthesis_set_chunk_blocks(pfb_synthesis_plan* plan, int32_t blocks);
 
+/* Where the fused round trip's synthesis gets its stage-1 rows (the channel IFFT of each
+ * channelised row = N^2 x the analysis FIR sums).  STORED: the analysis kernel writes them
+ * to the plan's scratch and the synthesis reads them back.  RECOMPUTED (N = 256 streaming
+ * shapes, Nf 256): the analysis writes only the channelised product and the synthesis
+ * evaluates the rows it needs from the input series — the same FIR sums in the same order,
+ * so the output is bit-identical, with the stage-1 rows never crossing HBM.  AUTO: the
+ * measured-faster one for the shape.  Shapes without a recomputing
+ * kernel use STORED whatever is set.  Reference: polyphase_analysis.m:88-121 and
+ * polyphase_synthesis.m:282-285 (the channel IFFT this factors). */
+typedef enum pfb_stage1_rows {
+  PFB_STAGE1_AUTO = 0,
+  PFB_STAGE1_STORED = 1,
+  PFB_STAGE1_RECOMPUTED = 2
+} pfb_stage1_rows;
+pfb_status pfb_synthesis_set_stage1_rows(pfb_synthesis_plan* plan, int32_t mode);
+
 /* ---------------------------------------------------------------- round trip */
 /* Analysis followed by synthesis of its output — replaces the analysis -> synthesis
  * sequence of test_data_pipeline.m:114,132 (and data_gen/pipeline.py:71-75).
@@ -224,9 +240,14 @@ pfb_status pfb_roundtrip_execute(pfb_analysis_plan* analysis, pfb_synthesis_plan
  * turns those rows into the output; n_dat and sample_offset must be the analysis half's.
  * The halves' results equal pfb_roundtrip_execute's fused path bit for bit.  The caller
  * orders them (synthesis after the analysis, the next analysis on the same pair after
- * the synthesis), e.g. with events.  PFB_ERR_UNSUPPORTED when the plans take the chunked
- * pipeline (see above); PFB_ERR_INVALID_ARG from the synthesis half when no rows of that
- * size were produced.  Reference: the same lines as pfb_roundtrip_execute. */
+ * the synthesis), e.g. with events.  With recomputed stage-1 rows
+ * (pfb_synthesis_set_stage1_rows) the analysis half writes no rows: the synthesis half
+ * re-reads `in`, which must stay allocated and unchanged until it has run.
+ * PFB_ERR_UNSUPPORTED when the plans take the chunked pipeline (see above);
+ * PFB_ERR_INVALID_ARG from the synthesis half when the plan holds no analysis half of this
+ * analysis plan with the same n_dat and sample_offset (another shape, another plan, or a
+ * whole round trip ran on the pair since).  Reference: the same lines as
+ * pfb_roundtrip_execute. */
 pfb_status pfb_roundtrip_analysis_execute(pfb_analysis_plan* analysis, pfb_synthesis_plan* synthesis,
                                           const pfb_cf32* in, int64_t in_pol_stride, int64_t n_dat,
                                           pfb_cf32* chan, int64_t chan_pol_stride, int64_t chan_capacity,

@@ -755,17 +755,21 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
     }
   }
   if (!a.scratch && !a.z) return hipErrorInvalidValue;
+  if (a.z_stage != 0 && !a.z) return hipErrorInvalidValue;
   // generic: FIR into scratch, then row FFT (with the padded circular time shift)
   const int64_t rows = a.K - a.row0;
   const int64_t total = rows * a.N;
   hipError_t e = hipSuccess;
-  if (!launch_fir_window(a, s, &e)) {
+  if (a.z_stage == 2) {
+    // (the FIR half ran before, into the same Z)
+  } else if (!launch_fir_window(a, s, &e)) {
     dim3 grid((unsigned)((total + NT - 1) / NT), (unsigned)a.n_pol);
     if (a.variant == kBunton) hipLaunchKernelGGL(fir_generic_kernel<kBunton>, grid, dim3(NT), 0, s, a);
     else hipLaunchKernelGGL(fir_generic_kernel<kPadded>, grid, dim3(NT), 0, s, a);
     e = hipGetLastError();
   }
   if (e != hipSuccess) return e;
+  if (a.z && a.z_stage == 1) return hipSuccess;
   if (a.z) {
     // round trip: the channelised rows come from the Z rows (already in output-row order,
     // N^2 x the FIR sums, index-reversed for the padded variant): the same row FFT on

@@ -219,6 +219,9 @@ struct pfb_analysis_plan {
   int64_t n_taps = 0;
   bool fused = false;
   DevBuf taps, twN, scratch;
+  // streaming shapes: the folded taps x N^2 [s][c][16] of analysis_stream_kernel, for the
+  // synthesis that recomputes the stage-1 rows (SynthBlockArgs::fir_g); empty otherwise
+  DevBuf gtab;
   DevBuf zrev;  // padded generic round trip: index reversal (N - i) mod N of the row FFT input
   // streaming (FilterBank.m:13-14 input_buffer / buffered_samples)
   DevBuf carry, work, stage_in, stage_out;
@@ -249,7 +252,8 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
                                float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
                                int64_t K_total, hipStream_t s, float2* z = nullptr,
                                int64_t z_ps = 0, int64_t z_row0 = 0, int64_t pad = 0,
-                               const OutLayout* lay = nullptr, int zblk = 0, const float2* pre = nullptr) {
+                               const OutLayout* lay = nullptr, int zblk = 0, const float2* pre = nullptr,
+                               int z_stage = 0) {
   if (K_end <= row0) return PFB_OK;
   if (p->variant == pfb::kLowCbf) {
     pfb::LowCbfArgs l{};
@@ -270,6 +274,7 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   }
   pfb::AnalysisArgs a = analysis_args(p, in, in_ps, n_dat, out, out_ps, row0, K_end, K_total, z, z_ps, z_row0,
                                       pad, lay, zblk, pre);
+  a.z_stage = z_stage;
   a.scratch = nullptr;
   if (!p->fused && !z) {
     HIPCHK(p->scratch.ensure((size_t)p->n_pol * (K_end - row0) * p->N * sizeof(float2)));
@@ -283,7 +288,8 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   // (with z: the stage-1 rows are a synthesis intermediate, not algorithmic bytes —
   // the synthesis' algorithmic read of its input is counted by the block kernel)
   const double bytes = (double)p->n_pol * (8.0 * in_samples + 8.0 * (K_end - row0) * p->N);
-  ProfScope ps(z ? 3 : 0, bytes, s, p->fused);  // generic path = FIR + row FFT launches
+  // generic path = FIR + row FFT launches (z_stage 1 / 2: one of them)
+  ProfScope ps(z ? 3 : 0, bytes, s, p->fused || z_stage != 0);
   HIPCHK(pfb::launch_analysis(a, s));
   return PFB_OK;
 }
@@ -441,6 +447,24 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
   for (int64_t i = 0; i < d->n_taps; ++i) taps[(size_t)i] = (float)d->taps[i];  // cast(filt, 'single')
   hipError_t e = upload(p->taps, taps);
   if (e == hipSuccess) e = upload(p->twN, twiddles(p->N, -1));
+  if (e == hipSuccess && analysis_emits_zblk(p) && p->N == 256) {
+    // g_s[m][c] = N^2 F[(m + 1) N + c - (s M mod N)], F = [N zeros, taps, zeros] — the
+    // streaming kernel's folded taps (pfb_ana_stream.hpp), scaled by the power of two N^2
+    // (exact), lags m < P + 1, zero-padded to 16 per (s, c)
+    const int N = p->N, PE = p->P + 1;
+    const float n2 = (float)N * (float)N;
+    std::vector<float> g((size_t)p->nu * N * 16, 0.f);
+    for (int sr = 0; sr < p->nu; ++sr) {
+      const int as = (int)(((int64_t)sr * p->M) % N);
+      for (int c = 0; c < N; ++c)
+        for (int m = 0; m < PE; ++m) {
+          const int j = (m + 1) * N + c - as;
+          const float f = (j >= N && j < (p->P + 1) * N) ? taps[(size_t)(j - N)] : 0.f;
+          g[((size_t)sr * N + c) * 16 + m] = n2 * f;
+        }
+    }
+    e = upload(p->gtab, g);
+  }
   if (e == hipSuccess && !p->fused && p->variant == pfb::kPadded) {
     std::vector<int> rev((size_t)p->N);
     for (int i = 0; i < p->N; ++i) rev[(size_t)i] = (p->N - i) % p->N;
@@ -460,6 +484,7 @@ pfb_status pfb_analysis_plan_destroy(pfb_analysis_plan* p) {
   p->taps.release();
   p->twN.release();
   p->zrev.release();
+  p->gtab.release();
   p->scratch.release();
   p->carry.release();
   p->work.release();
@@ -710,6 +735,7 @@ struct pfb_synthesis_plan {
   int W = 0, keep = 0, L = 0, Lov = 0, Lkeep = 0, t1_lo = 0, t1_hi = 0;
   bool deripple = false;
   int chunk_blocks = 0;
+  int stage1 = PFB_STAGE1_AUTO;  // pfb_synthesis_set_stage1_rows
   int rt_chunk_blocks = 64;  // round-trip pipeline chunk (PFB_RT_CHUNK_BLOCKS)
   int timing_mask = 0;  // PFB_TIMING_MASK (timing experiments; results invalid when set)
   int ranges = -1;  // PFB_SYNTH_RANGES: 0 one workgroup per block, -1 persistent auto, >0 persistent
@@ -727,12 +753,28 @@ struct pfb_synthesis_plan {
   // written by anything else
   uint64_t zkey_plan = 0;
   int64_t zkey[5] = {-1, -1, -1, -1, -1};
+  // (recomputed rows: the analysis half left no rows, only the input the synthesis reads)
+  const void* zkey_x = nullptr;
+  int64_t zkey_xps = -1;
 };
+
+// PFB_STAGE1_AUTO: recomputed stage-1 rows in the Nf = 256 round trip
+constexpr bool kSynthFirDefault = false;
 
 static void zkey_clear(pfb_synthesis_plan* p) {
   p->zkey_plan = 0;
   std::fill(p->zkey, p->zkey + 5, (int64_t)-1);
+  p->zkey_x = nullptr;
+  p->zkey_xps = -1;
 }
+
+// the input series a synthesis recomputes its stage-1 rows from (SynthBlockArgs::fir_*)
+struct FirSrc {
+  const float2* x;
+  int64_t x_ps, n_dat, q0;
+  const float* g;
+  int nu, de, pe;
+};
 
 static void hann_sym(int L, std::vector<double>& h) {
   h.resize((size_t)L);
@@ -750,7 +792,7 @@ static int64_t synth_blocks(const pfb_synthesis_plan* p, int64_t n_dat) {
 
 static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64_t z_ps, int64_t b0,
                                    int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
-                                   hipStream_t s, int zblk = 0);
+                                   hipStream_t s, int zblk = 0, const FirSrc* fir = nullptr);
 
 // Blocks [b0, b0 + nb) with a spectral taper (pfb_spectral.hip): Matlab's order — per
 // channel FFT, stitch x taper, then the L-point IFFT as row FFTs — in sub-chunks whose
@@ -836,8 +878,18 @@ static pfb_status synthesis_chunk(pfb_synthesis_plan* p, const float2* in, int64
 // Block kernel over blocks [b0, b0 + nb); Z row 0 is channelised row b0 * keep.
 static pfb::SynthBlockArgs synth_args(const pfb_synthesis_plan* p, const float2* Z, int64_t z_ps,
                                       int64_t b0, int64_t nb, float2* out, int64_t out_ps,
-                                      int64_t out_limit, int zblk = 0) {
+                                      int64_t out_limit, int zblk = 0, const FirSrc* fir = nullptr) {
   pfb::SynthBlockArgs a{};
+  if (fir) {
+    a.fir_x = fir->x;
+    a.fir_x_pol_stride = fir->x_ps;
+    a.fir_n_dat = fir->n_dat;
+    a.fir_g = fir->g;
+    a.fir_q0 = fir->q0;
+    a.fir_nu = fir->nu;
+    a.fir_de = fir->de;
+    a.fir_pe = fir->pe;
+  }
   a.Z = Z;
   a.z_pol_stride = z_ps;
   a.out = out;
@@ -872,8 +924,8 @@ static pfb::SynthBlockArgs synth_args(const pfb_synthesis_plan* p, const float2*
 
 static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64_t z_ps, int64_t b0,
                                    int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
-                                   hipStream_t s, int zblk) {
-  const pfb::SynthBlockArgs a = synth_args(p, Z, z_ps, b0, nb, out, out_ps, out_limit, zblk);
+                                   hipStream_t s, int zblk, const FirSrc* fir) {
+  const pfb::SynthBlockArgs a = synth_args(p, Z, z_ps, b0, nb, out, out_ps, out_limit, zblk, fir);
   {
     ProfScope ps(2, (double)p->n_pol * (nb * p->keep * p->N * 8.0 + nb * p->Lkeep * 8.0), s);
     HIPCHK(pfb::launch_synth_block(a, s));
@@ -1155,6 +1207,15 @@ int64_t pfb_synthesis_output_length(const pfb_synthesis_plan* p, int64_t n_dat) 
   return synth_blocks(p, n_dat) * p->Lkeep;
 }
 
+pfb_status pfb_synthesis_set_stage1_rows(pfb_synthesis_plan* p, int32_t mode) {
+  if (!p) return fail(PFB_ERR_INVALID_ARG, "null plan");
+  if (mode != PFB_STAGE1_AUTO && mode != PFB_STAGE1_STORED && mode != PFB_STAGE1_RECOMPUTED)
+    return fail(PFB_ERR_INVALID_ARG, "unknown stage-1 row mode %d", mode);
+  p->stage1 = mode;
+  zkey_clear(p);  // a split round trip in flight is not continued under another mode
+  return PFB_OK;
+}
+
 pfb_status pfb_synthesis_set_chunk_blocks(pfb_synthesis_plan* p, int32_t blocks) {
   if (!p) return fail(PFB_ERR_INVALID_ARG, "null plan");
   p->chunk_blocks = std::max(0, blocks);
@@ -1401,7 +1462,48 @@ static pfb_status roundtrip_run(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, c
   const size_t zbytes = (size_t)pa->n_pol * zrows * pa->N * sizeof(float2);
   bool fuse = !no_fuse && analysis_emits_z(pa) && ps->identity_perm && !ps->has_cgain &&
               !ps->has_spectral && ps->chunk_blocks <= 0 && zbytes <= ((size_t)16 << 30);
-  const int64_t zkey[5] = {n_dat, off, zblk, K, zrows};
+  // Recomputed stage-1 rows (SynthBlockArgs::fir_x): the analysis writes only the
+  // channelised product and the synthesis evaluates the rows it needs from the input
+  // series — the same FIR sums, bit for bit (555 instead of 727 MB of HBM traffic per C2
+  // step).  Where the wave kernel takes the run layout (zblk) and has a FIR variant
+  // (pfb_synthesis_set_stage1_rows).
+  const bool synth_fir_on = ps->stage1 == PFB_STAGE1_RECOMPUTED || (ps->stage1 == PFB_STAGE1_AUTO && kSynthFirDefault);
+  FirSrc fsrc{(const float2*)in, in_ps, n_dat, off / std::max(pa->nu, 1), pa->gtab.as<float>(), pa->nu, pa->de,
+              pa->P + 1};
+  bool fir = false;
+  if (synth_fir_on && zblk && pa->gtab.p && off % pa->nu == 0 && phase != 2) {
+    fir = pfb::synth_wave_fir_supported(synth_args(ps, nullptr, 0, 0, B, nullptr, 0, 0, 0, &fsrc));
+  }
+  if (phase == 2 && ps->zkey_x != nullptr) {
+    // the analysis half chose recomputed rows: the synthesis reads the input it recorded
+    fir = true;
+    fsrc.x = (const float2*)ps->zkey_x;
+    fsrc.x_ps = ps->zkey_xps;
+  }
+  const int64_t zkey[5] = {n_dat, off, fir ? -1 : zblk, K, zrows};
+  if (fir && fuse) {
+    if (phase == 2) {
+      if (ps->zkey_plan != pa->serial || !std::equal(zkey, zkey + 5, ps->zkey))
+        return fail(PFB_ERR_INVALID_ARG,
+                    "split round trip: the synthesis plan holds no analysis half of this analysis plan, "
+                    "n_dat %lld and sample_offset %lld (run pfb_roundtrip_analysis_execute with the same "
+                    "arguments first)",
+                    (long long)n_dat, (long long)sample_offset);
+      return synthesis_blocks(ps, nullptr, 0, 0, B, (float2*)out, out_ps, olen, s, 0, &fsrc);
+    }
+    zkey_clear(ps);
+    pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s);
+    if (st != PFB_OK) return st;
+    if (phase == 1) {
+      // the synthesis half re-reads this input: the caller keeps it unchanged until then
+      ps->zkey_plan = pa->serial;
+      std::copy(zkey, zkey + 5, ps->zkey);
+      ps->zkey_x = in;
+      ps->zkey_xps = in_ps;
+      return PFB_OK;
+    }
+    return synthesis_blocks(ps, nullptr, 0, 0, B, (float2*)out, out_ps, olen, s, 0, &fsrc);
+  }
   if (fuse && phase == 2) {
     // the synthesis half reads the rows the analysis half left in the plan's scratch: they
     // must come from this analysis plan with the same n_dat, offset and row layout
@@ -1444,6 +1546,32 @@ static pfb_status roundtrip_run(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, c
     float2* Z = ps->Z.as<float2>();
     static const int conc = pfb::knob("PFB_RT_CONC") ? std::atoi(pfb::knob("PFB_RT_CONC")) : 1;
     const int64_t C = std::min<int64_t>(std::max(conc, 1), B);
+    // generic (N > 256) path: the row FFT (Z -> channelised rows) and the synthesis (Z ->
+    // output) both read Z and are independent, so the row FFT may run on the analysis
+    // plan's stream beside the synthesis (PFB_RT_ROWFFT_CONC=1, experiments A/B)
+    static const bool rowfft_conc = pfb::knob("PFB_RT_ROWFFT_CONC") && std::atoi(pfb::knob("PFB_RT_ROWFFT_CONC")) == 1;
+    if (!pa->fused && rowfft_conc) {
+      pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0,
+                                   nullptr, zblk, nullptr, 1);
+      if (st != PFB_OK) return st;
+      if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));
+      while (pa->events.size() < 2) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        pa->events.push_back(e);
+      }
+      HIPCHK(hipEventRecord(pa->events[0], s));
+      HIPCHK(hipStreamWaitEvent(pa->aux, pa->events[0], 0));
+      st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, pa->aux, Z, zrows * pa->N, z0, 0, nullptr,
+                        zblk, nullptr, 2);
+      if (st != PFB_OK) return st;
+      st = synthesis_blocks(ps, Z + (off - z0) * pa->N, zrows * pa->N, 0, B, (float2*)out, out_ps, olen, s,
+                            zblk);
+      if (st != PFB_OK) return st;
+      HIPCHK(hipEventRecord(pa->events[1], pa->aux));
+      HIPCHK(hipStreamWaitEvent(s, pa->events[1], 0));
+      return PFB_OK;
+    }
     if (C <= 1 || !zblk) {
       pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0,
                                    nullptr, zblk);

@@ -78,6 +78,10 @@ struct AnalysisArgs {
   // consecutive rows of one column are one run; needs (row0 - z_row0) % 16 == 0
   // (launch_analysis checks); 0 or 1: rows [row][c]
   int zblk;
+  // generic path (N > 256) with z: 0 both launches; 1 only the FIR (Z rows); 2 only the
+  // row FFT (channelised rows from Z) — so the row FFT can run beside the synthesis, which
+  // reads the same Z rows
+  int z_stage;
 };
 // SKA-Low CBF PST filterbank through the streaming analysis kernel (pfb_analysis.hip)
 hipError_t launch_lowcbf_stream(const AnalysisArgs& a, hipStream_t s);
@@ -129,6 +133,17 @@ struct SynthBlockArgs {
   int timing_mask;         // experiments build only (PFB_TIMING_MASK, results invalid): bit0
                            // drop Z loads, bit1 drop output stores, bit2 drop tw4 loads
   int zblk;                // Z layout of AnalysisArgs::zblk (0/1 rows, else ZB-row runs)
+  // Recomputed stage-1 rows (the Nf = 256 round trip, synth_wave_kernel with fir_x set): the
+  // analysis writes no Z; the synthesis evaluates each row it needs as N^2 x the streaming
+  // analysis's FIR sums of the input series itself (same taps, same FMA order: bit-identical
+  // rows).  fir_g[(s N + c) 16 + m] = N^2 x the folded tap of residue s, lag m < PE, column c
+  // (pfb_ana_stream.hpp); Z row j is analysis row NU fir_q0 + j.
+  const float2* fir_x;     // [pol][t] input series (null: read Z)
+  int64_t fir_x_pol_stride;
+  int64_t fir_n_dat;
+  const float* fir_g;
+  int64_t fir_q0;
+  int fir_nu, fir_de, fir_pe;
 };
 
 // Synthesis with a non-identity spectral taper (pfb_spectral.hip): blocks [b0, b0 + nb)
@@ -196,6 +211,8 @@ bool synth_block_supported(int Nf, int W);
 // Nf = 256 synthesis with one output phase per 16 lanes and no barrier in the block loop
 // (pfb_synth_wave.hip); launch_synth_block takes it where it applies
 bool synth_wave_supported(const SynthBlockArgs& a);
+// the same kernel with recomputed stage-1 rows (SynthBlockArgs::fir_x)
+bool synth_wave_fir_supported(const SynthBlockArgs& a);
 hipError_t launch_synth_wave(const SynthBlockArgs& a, hipStream_t s);
 // Nf = 512, W = 448, keep 256 (SKA-Mid): one output phase per 32 lanes (pfb_synth_wave512.hip)
 bool synth_wave512_supported(const SynthBlockArgs& a);

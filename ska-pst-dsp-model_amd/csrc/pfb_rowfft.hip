@@ -17,7 +17,11 @@ static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s
     static const bool off = knob("PFB_ROWFFT_PERSIST") && std::atoi(knob("PFB_ROWFFT_PERSIST")) == 0;
     const size_t bytes = ((size_t)RowShape<N>::RS + tw_slots(N)) * sizeof(float2);
     const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / bytes);
-    const int64_t wgs = (int64_t)cu_count() * per_cu;
+    int64_t wgs = (int64_t)cu_count() * per_cu;
+    // (PFB_ROWFFT_WGS: fewer persistent workgroups, so the row FFT can share the chip with
+    // a concurrent synthesis — experiments A/B)
+    static const int env_wgs = knob("PFB_ROWFFT_WGS") ? std::atoi(knob("PFB_ROWFFT_WGS")) : 0;
+    if (env_wgs > 0) wgs = env_wgs;
     if (!off && r.n_rows >= 4 * wgs) {
       auto kern = row_fft_persist_kernel<N, DIR, PERM, GAIN>;
       hipError_t e = set_lds(kern, bytes);

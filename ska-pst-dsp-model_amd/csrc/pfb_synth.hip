@@ -237,7 +237,7 @@ bool synth_block_supported(int Nf, int W) {
 hipError_t launch_synth_block(const SynthBlockArgs& a, hipStream_t s) {
   if (a.n_blocks <= 0) return hipSuccess;
   // stage-1 rows for the wave kernel (the fused round trip, Nf = 256: zblk = run length)
-  if (a.zblk) return launch_synth_wave(a, s);
+  if (a.zblk || a.fir_x) return launch_synth_wave(a, s);
   // SKA-Mid shape (Nf 512, W 448, Ov 128): the wave kernel (PFB_SYNTH_WAVE512=0: the block
   // kernel, experiments build)
   static const bool no_w5 = knob("PFB_SYNTH_WAVE512") && std::atoi(knob("PFB_SYNTH_WAVE512")) == 0;

@@ -34,12 +34,24 @@ namespace pfb {
 bool synth_wave_supported(const SynthBlockArgs& a) {
   if (a.Nf != 256 || (a.W != 224 && a.W != 192)) return false;
   if (a.N % kCols != 0) return false;
+  if (a.fir_x) return synth_wave_fir_supported(a);
   return (a.zblk == 1 || a.zblk == 2 || a.zblk == 4) && a.keep == 160;
 }
 
-template <int RW, bool SPANS, bool XW>
+// recomputed stage-1 rows: the streaming analysis shapes (N 256; 8/7 with W 224, 4/3 with
+// W 192; P 12 or 13 -> PE 13 or 14 folded taps) and input offsets within one descriptor
+bool synth_wave_fir_supported(const SynthBlockArgs& a) {
+  if (a.Nf != 256 || a.keep != 160 || a.N != 256 || !a.fir_x || !a.fir_g) return false;
+  const bool s87 = a.W == 224 && a.fir_nu == 8 && a.fir_de == 7;
+  const bool s43 = a.W == 192 && a.fir_nu == 4 && a.fir_de == 3;
+  if (!(s87 || s43) || (a.fir_pe != 13 && a.fir_pe != 14) || a.fir_q0 < 0) return false;
+  // tile offsets of the last block stay below 2^31 bytes
+  return (a.fir_n_dat + 512 * (int64_t)a.N) * 8 < kRsrcMaxBytes;
+}
+
+template <int RW, bool SPANS, bool XW, class FIRV = NoFir>
 static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
-  auto kern = synth_wave_kernel<RW, SPANS, 10, XW>;
+  auto kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV>;
   hipError_t e = set_lds(kern, kLdsB);
   if (e != hipSuccess) return e;
   const int groups = a.N / kCols;
@@ -53,9 +65,19 @@ static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
   return launch_kernel(kern, grid, dim3(kWgThreads), kLdsB, s, a);
 }
 
+template <int RW, int NU, int DE>
+static hipError_t launch_wave_fir(const SynthBlockArgs& a, hipStream_t s) {
+  if (a.fir_pe == 14)
+    return a.spans ? launch_wave_t<RW, true, false, FirShape<NU, DE, 14>>(a, s)
+                   : launch_wave_t<RW, false, false, FirShape<NU, DE, 14>>(a, s);
+  return a.spans ? launch_wave_t<RW, true, false, FirShape<NU, DE, 13>>(a, s)
+                 : launch_wave_t<RW, false, false, FirShape<NU, DE, 13>>(a, s);
+}
+
 hipError_t launch_synth_wave(const SynthBlockArgs& a, hipStream_t s) {
   if (a.n_blocks <= 0) return hipSuccess;
   if (!synth_wave_supported(a)) return hipErrorInvalidValue;
+  if (a.fir_x) return a.W == 224 ? launch_wave_fir<14, 8, 7>(a, s) : launch_wave_fir<12, 4, 3>(a, s);
   // pass-1 lanes spread over the workgroup (synthesis 78.5-80.2 -> 74.2-75.1 us on C2,
   // profiles/r03_v8_c2_wave_xw_ab.jsonl); PFB_WAVE_XW=0: within the wave (experiments A/B)
   static const bool xw = !(knob("PFB_WAVE_XW") && std::atoi(knob("PFB_WAVE_XW")) == 0);

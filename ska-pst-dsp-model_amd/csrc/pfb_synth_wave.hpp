@@ -52,6 +52,32 @@ constexpr int bin_of(int rr) {
 
 }  // namespace
 
+// Stage-1 rows read from Z (the streaming analysis wrote them)
+struct NoFir {
+  static constexpr bool kOn = false;
+  static constexpr int NU = 1, DE = 1, PE = 1, S = 1, RS = 0;
+  static constexpr int rows(int) { return 0; }
+  static constexpr int loads(int) { return 1; }
+};
+// Stage-1 rows recomputed from the input series (SynthBlockArgs::fir_x): lane (l, col) of
+// pass 1 needs Z rows k = NU q0 + keep b + l + 16 r of phase c = t0g + col, i.e. residue
+// s = l mod NU and commutator step q = q0 + (keep / NU) b + l / NU + (16 / NU) r, whose FIR
+// sum (pfb_ana_stream.hpp) is sum_m g_s[m][c] X[DE q + b_s + m][c] over PE taps, X the
+// input as rows of N.  So row r of the lane reads input rows T0(b) + o_l + S r + m with
+// T0(b) = DE (q0 + (keep / NU) b), o_l = DE (l / NU) + b_s, S = 16 DE / NU: the workgroup's
+// 16 columns of those rows go through an LDS tile (rows of RS bytes; the reads of one
+// 32-lane group hit 8 distinct rows x 4 columns, spread over the banks by the 32-B pad).
+template <int NU_, int DE_, int PE_>
+struct FirShape {
+  static constexpr bool kOn = true;
+  static constexpr int NU = NU_, DE = DE_, PE = PE_;
+  static constexpr int S = DE * 16 / NU;
+  static constexpr int OMAX = DE * (16 / NU - 1) + ((NU - 1) * DE) / NU;  // largest o_l
+  static constexpr int RS = 160;
+  static constexpr int rows(int r_lo) { return OMAX + (15 - r_lo) * S + PE; }  // tile rows for r >= r_lo
+  static constexpr int loads(int r_lo) { return (rows(r_lo) + 31) / 32; }      // 16-B loads per thread
+};
+
 // The workgroup's blocks: a contiguous range, each block's first 16 - DK register rows
 // taken from the previous block.  (A schedule class, so that a producer-consumer launch can
 // supply blocks in the order their rows are ready and wait for each — the one-launch
@@ -71,11 +97,13 @@ struct RangeSched {
 // in wave l / 4): one Z load instruction reads 2 row pairs x the 16 phases (256-B runs)
 // instead of 8 row pairs x 4 phases (64-B runs), and swap 1 crosses waves (one more
 // workgroup barrier per block)
-template <int RW, bool SPANS, int DK, class SCHED, bool XW = false>
+template <int RW, bool SPANS, int DK, class SCHED, bool XW = false, class FIRV = NoFir>
 __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol, int tg, const SCHED& sch) {
   constexpr int W = 16 * RW;
   static_assert(RW <= 14 && RW % 2 == 0, "W = 16 RW with RW even and <= 14");
   static_assert(DK >= 1 && DK <= 16, "keep = 16 DK");
+  static_assert(!FIRV::kOn || !XW, "the FIR synthesis uses the in-wave pass-1 mapping");
+  static_assert(!FIRV::kOn || FIRV::rows(0) <= kTilesB / 160, "FIR tile exceeds the phase tiles");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -139,6 +167,72 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
   float2* opol = a.out + pol * a.out_pol_stride;
 
   float2 x[16];  // raw Z values of the next block, rows l + 16 r
+
+  // ---- FIR synthesis (FIRV::kOn): the lane's folded taps, its tile row offset, the input
+  constexpr int NU = FIRV::NU, DE = FIRV::DE, PE = FIRV::PE, S = FIRV::kOn ? FIRV::S : 1;
+  constexpr int RL = 16 - DK;  // first register row a later block computes (the others are reused)
+  // (the taps are re-read from the L1/L2-resident table for every block: kept in registers
+  // across the FFT passes they would push the kernel past the 168-VGPR budget of 3 waves
+  // per SIMD)
+  [[maybe_unused]] float g[PE];
+  [[maybe_unused]] int fir_o = 0;
+  [[maybe_unused]] const float* gl = nullptr;
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t xr =
+      FIRV::kOn ? make_rsrc(a.fir_x + pol * a.fir_x_pol_stride, (uint32_t)min(a.fir_n_dat * 8, (int64_t)kRsrcMaxBytes))
+                : make_rsrc(a.Z, 0u);
+  if constexpr (FIRV::kOn) {
+    const int sr = l % NU;
+    fir_o = DE * (l / NU) + (sr * DE) / NU;
+    gl = a.fir_g + ((int64_t)sr * N + t0g + col) * 16;
+  }
+  auto load_taps = [&]() {  // the lane's PE taps: 16 contiguous floats, 4 x 16-B loads
+    static_for<0, 4>([&](auto k) {
+      const v4f q = *reinterpret_cast<const v4f*>(gl + 4 * decltype(k)::value);
+      static_for<0, 4>([&](auto e) {
+        constexpr int m = 4 * decltype(k)::value + decltype(e)::value;
+        if constexpr (m < PE) g[m] = q[decltype(e)::value];
+      });
+    });
+  };
+  // input rows T0(b) + S r_lo + j (j = tid / 8 + 32 i), 16 B of the workgroup's 16 columns each
+  auto tile_load = [&](int b, auto r_lo, v4u* pf) {
+    constexpr int NL = FIRV::loads(decltype(r_lo)::value);
+    const int64_t row0 = (int64_t)DE * (a.fir_q0 + (int64_t)(a.keep / NU) * b) + S * decltype(r_lo)::value;
+    uint32_t o = (uint32_t)(((row0 + (tid >> 3)) * N + t0g + 2 * (tid & 7)) * 8);
+    asm volatile("" : "+v"(o));  // (no per-load offsets hoisted out of the block loop)
+    static_for<0, NL>([&](auto i) {
+      pf[decltype(i)::value] =
+          __builtin_amdgcn_raw_buffer_load_b128(xr, o + (uint32_t)(decltype(i)::value * 32 * N * 8), 0, 0);
+    });
+  };
+  auto tile_store = [&](auto r_lo, const v4u* pf) {
+    constexpr int NL = FIRV::loads(decltype(r_lo)::value);
+    static_for<0, NL>([&](auto i) {
+      const int j = (tid >> 3) + 32 * decltype(i)::value;
+      *reinterpret_cast<v4u*>(lds + j * FIRV::RS + 16 * (tid & 7)) = pf[decltype(i)::value];
+    });
+  };
+  // x[r], r >= r_lo, from the tile (tile row 0 = input row T0(b) + S r_lo); the FMA order of
+  // the streaming analysis (m ascending from 0) with N^2-scaled taps: N^2 x its sums exactly
+  auto fir_rows = [&](auto r_lo) {
+    constexpr int R_LO = decltype(r_lo)::value;
+    const char* tb = lds + fir_o * FIRV::RS + col * 8;
+    v2f acc[16 - R_LO];
+    static_for<0, 16 - R_LO>([&](auto rv) { acc[decltype(rv)::value] = v2f{0.f, 0.f}; });
+    static_for<0, PE>([&](auto mv) {
+      constexpr int m = decltype(mv)::value;
+      static_for<0, 16 - R_LO>([&](auto rv) {
+        constexpr int rr = decltype(rv)::value;
+        const v2f xv = *reinterpret_cast<const v2f*>(tb + (rr * S + m) * FIRV::RS);
+        acc[rr] = __builtin_elementwise_fma(v2f{g[m], g[m]}, xv, acc[rr]);
+      });
+    });
+    static_for<0, 16 - R_LO>([&](auto rv) {
+      constexpr int rr = decltype(rv)::value;
+      x[R_LO + rr] = make_float2(acc[rr].x, acc[rr].y);
+    });
+  };
+
   auto prefetch = [&](int b, auto reuse) {
     constexpr int R0 = decltype(reuse)::value ? 16 - DK : 0;
     static_for<0, R0>([&](auto r) { x[r] = x[r + DK]; });
@@ -148,7 +242,18 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       x[r] = __builtin_bit_cast(float2, v);
     });
   };
-  prefetch(sch.block(0), std::false_type{});
+  [[maybe_unused]] v4u pf[FIRV::kOn ? FIRV::loads(RL) : 1];
+  if constexpr (FIRV::kOn) {
+    // first block: all 16 register rows from one tile (the phase tiles are not in use yet)
+    v4u pf0[FIRV::loads(0)];
+    tile_load(sch.block(0), std::integral_constant<int, 0>{}, pf0);
+    load_taps();
+    tile_store(std::integral_constant<int, 0>{}, pf0);
+    __syncthreads();
+    fir_rows(std::integral_constant<int, 0>{});
+  } else {
+    prefetch(sch.block(0), std::false_type{});
+  }
 
 #pragma unroll 1
   for (int i = 0; i < nb; ++i) {
@@ -173,7 +278,10 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       static_for<0, 16>([&](auto r) { v[r] = cscale(x[r], wv[r]); });
     }
     // the next block's rows (the last block re-reads itself: the wait count stays fixed)
-    prefetch(sch.block(min(i + 1, nb - 1)), std::integral_constant<bool, (SCHED::kReuse && DK < 16)>{});
+    if constexpr (FIRV::kOn)
+      tile_load(sch.block(min(i + 1, nb - 1)), std::integral_constant<int, RL>{}, pf);
+    else
+      prefetch(sch.block(min(i + 1, nb - 1)), std::integral_constant<bool, (SCHED::kReuse && DK < 16)>{});
     sdft<16, -1>(v);
     {
       float2 w[16];
@@ -224,16 +332,32 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       const __amdgpu_buffer_rsrc_t o = make_rsrc(opol + ob, (uint32_t)nk * 8u);
       // lanes t1a >= RW hold no output: their offsets leave the descriptor's range (as do
       // the discarded t1 < t1_lo, whose negative offsets wrap past 2^31)
-      const int base = (t1a < RW) ? ((t1a - a.t1_lo) * N + t0g + col2) * 8 : (int)0x80000000;
+      int base = (t1a < RW) ? ((t1a - a.t1_lo) * N + t0g + col2) * 8 : (int)0x80000000;
+      // (FIR variant: recomputed every block — 16 hoisted store offsets would spill)
+      if constexpr (FIRV::kOn) asm volatile("" : "+v"(base));
       static_for<0, 16>([&](auto t) {
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v[t]), o,
                                               (uint32_t)(base + t * RW * N * 8), 0, 0);
       });
     }
+    if constexpr (FIRV::kOn) {
+      if (i + 1 < nb) {  // uniform per workgroup
+        // the next block: its first RL register rows are this block's last, the others come
+        // from the input rows loaded above, staged in the phase tiles once every wave has
+        // read its swap-2 data (the next iteration's first barrier orders the FIR reads
+        // before that block's swap 1)
+        static_for<0, RL>([&](auto r) { x[decltype(r)::value] = x[decltype(r)::value + DK]; });
+        __syncthreads();
+        load_taps();
+        tile_store(std::integral_constant<int, RL>{}, pf);
+        __syncthreads();
+        fir_rows(std::integral_constant<int, RL>{});
+      }
+    }
   }
 }
 
-template <int RW, bool SPANS, int DK, bool XW = false>
+template <int RW, bool SPANS, int DK, bool XW = false, class FIRV = NoFir>
 __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(3)))
 void synth_wave_kernel(SynthBlockArgs a) {
   const int groups = a.N / kCols;
@@ -242,7 +366,8 @@ void synth_wave_kernel(SynthBlockArgs a) {
   const int Rg = gridDim.x / groups;
   const int b_begin = (int)((int64_t)a.n_blocks * rr / Rg);
   const int b_end = (int)((int64_t)a.n_blocks * (rr + 1) / Rg);
-  synth_wave_body<RW, SPANS, DK, RangeSched, XW>(a, blockIdx.y, lt % groups, RangeSched{b_begin, b_end - b_begin});
+  synth_wave_body<RW, SPANS, DK, RangeSched, XW, FIRV>(a, blockIdx.y, lt % groups,
+                                                       RangeSched{b_begin, b_end - b_begin});
 }
 
 }  // namespace pfb

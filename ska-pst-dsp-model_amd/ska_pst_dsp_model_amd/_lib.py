@@ -36,6 +36,9 @@ PFB_WINDOW_TOP_HAT = 2
 PFB_WINDOW_HANN = 3
 PFB_WINDOW_CUSTOM = 4
 
+PFB_STAGE1_AUTO = 0
+PFB_STAGE1_STORED = 1
+PFB_STAGE1_RECOMPUTED = 2
 PFB_DADA_TFP = 0
 PFB_DADA_LOWCBF = 1
 
@@ -96,6 +99,7 @@ SYMBOLS = [
     ("pfb_inverse_filterbank_buffered", c_int64, [c_void_p]),
     ("pfb_inverse_filterbank_reset", c_int32, [c_void_p]),
     ("pfb_synthesis_set_chunk_blocks", c_int32, [c_void_p, c_int32]),
+    ("pfb_synthesis_set_stage1_rows", c_int32, [c_void_p, c_int32]),
     ("pfb_roundtrip_execute", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                         c_void_p, c_int64, c_int64, POINTER(c_int64), c_int64,
                                         c_void_p, c_int64, c_int64, POINTER(c_int64), c_void_p]),

@@ -318,6 +318,16 @@ class SynthesisPlan:
     def set_chunk_blocks(self, blocks: int):
         _lib.check(self._lib.pfb_synthesis_set_chunk_blocks(self._h, int(blocks)))
 
+    STAGE1_ROWS = {"auto": _lib.PFB_STAGE1_AUTO, "stored": _lib.PFB_STAGE1_STORED,
+                   "recomputed": _lib.PFB_STAGE1_RECOMPUTED}
+
+    def set_stage1_rows(self, mode: str):
+        """Round trip only (pfb_synthesis_set_stage1_rows): 'stored' — the analysis writes
+        the synthesis stage-1 rows and the synthesis reads them; 'recomputed' — the
+        synthesis evaluates them from the input series (N = 256 streaming shapes;
+        bit-identical output); 'auto' — the measured-faster one."""
+        _lib.check(self._lib.pfb_synthesis_set_stage1_rows(self._h, self.STAGE1_ROWS[mode]))
+
     def output_length(self, n_dat: int) -> int:
         return int(self._lib.pfb_synthesis_output_length(self._h, int(n_dat)))
 

@@ -598,3 +598,77 @@ def test_mid_external_matches_oracle(gpu):
     assert ref.shape == (1, 1, 5 * (917504 - 2 * 114688))
     assert_pfb_close(out.cpu().numpy()[:, None, :], ref, scale=1.0,
                      what="mid_external round trip (raw)")
+
+
+# ------------------------------------------------------------------ recomputed stage-1 rows
+@pytest.mark.parametrize("os_,tpc,n,so,n_pol", [
+    ("8/7", 12, 1 << 20, 1, 1),        # C2 shape (P 13)
+    ("8/7", 11, 1 << 20, 17, 2),       # P 12, offset, two polarisations
+    ("4/3", 12, 1 << 20, 1, 1),        # C2' shape ('low')
+    ("4/3", 11, 777_777, 33, 2),       # ragged length, offset
+    ("8/7", 12, 1 << 24, 1, 1),        # full C2 unit
+])
+def test_roundtrip_recomputed_stage1_rows_bit_identical(gpu, os_, tpc, n, so, n_pol):
+    """pfb_synthesis_set_stage1_rows(RECOMPUTED): the synthesis evaluates the stage-1 rows
+    from the input (the analysis writes only the channelised product).  The rows are the
+    same FIR sums in the same FMA order with taps pre-scaled by N^2 (a power of two), so
+    the channelised product and the output equal the stored-rows round trip bit for bit —
+    whole calls and split halves (the synthesis half re-reads the input)."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, os_, tpc)
+    win = pfb.PFBWindow().lookup["tukey"](256, 48)
+    x = _noise_t(torch, gpu, (n_pol, n), 31)
+
+    def pair(mode):
+        a = pfb.AnalysisPlan(taps, 256, os_, "polyphase_analysis", n_pol, 0)
+        s = pfb.SynthesisPlan(256, os_, 256, 48, True, 1, True, taps, win, None, n_pol, 0)
+        s.set_stage1_rows(mode)
+        return a, s
+    a0, s0 = pair("stored")
+    c_ref, o_ref = pfb.roundtrip(a0, s0, x, sample_offset=so)
+    a1, s1 = pair("recomputed")
+    c1, o1 = pfb.roundtrip(a1, s1, x, sample_offset=so)
+    torch.cuda.synchronize()
+    assert torch.equal(c1, c_ref)
+    assert torch.equal(o1, o_ref)
+    # split halves on two streams
+    chan = pfb.roundtrip_analysis(a1, s1, x, sample_offset=so)
+    ss = torch.cuda.Stream()
+    ss.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(ss):
+        out = pfb.roundtrip_synthesis(a1, s1, x.shape[1], sample_offset=so, device=gpu.index or 0)
+    torch.cuda.synchronize()
+    assert torch.equal(chan, c_ref)
+    assert torch.equal(out, o_ref)
+    # the analysis half of one mode is not continued by the other
+    pfb.roundtrip_analysis(a1, s1, x, sample_offset=so)
+    s1.set_stage1_rows("stored")
+    with pytest.raises(pfb.PfbError):
+        pfb.roundtrip_synthesis(a1, s1, x.shape[1], sample_offset=so, device=gpu.index or 0)
+
+
+def test_roundtrip_recomputed_rows_reject_mismatch(gpu):
+    """The recomputed-rows synthesis half checks the analysis plan, n_dat and offset of the
+    analysis half, as the stored-rows one does."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
+    win = pfb.PFBWindow().lookup["tukey"](256, 48)
+    x = _noise_t(torch, gpu, (1, 1 << 19), 37)
+    a = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
+    b = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
+    s = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, 1, 0)
+    s.set_stage1_rows("recomputed")
+    dev = gpu.index or 0
+    pfb.roundtrip_analysis(a, s, x)
+    with pytest.raises(pfb.PfbError):
+        pfb.roundtrip_synthesis(a, s, x.shape[1] - 2048, device=dev)
+    with pytest.raises(pfb.PfbError):
+        pfb.roundtrip_synthesis(b, s, x.shape[1], device=dev)
+    with pytest.raises(pfb.PfbError):
+        pfb.roundtrip_synthesis(a, s, x.shape[1], sample_offset=17, device=dev)
+    out = pfb.roundtrip_synthesis(a, s, x.shape[1], device=dev)
+    _, o_ref = pfb.roundtrip(b, s, x)
+    torch.cuda.synchronize()
+    assert torch.equal(out, o_ref)
