@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--only-mid", action="store_true")
     ap.add_argument("--only-twostage", action="store_true")
     ap.add_argument("--inflight", type=int, default=1, help="C3 units in flight (plan pairs/streams)")
+    ap.add_argument("--graph", type=int, default=1, help="with --pipeline: capture the steps as one graph")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="with --inflight > 1: the split round trip pipelined over two streams")
     ap.add_argument("--cpu", action="store_true",
@@ -66,7 +67,8 @@ def main():
     if args.cpu:
         cpu_baselines(pfb)
     if args.only_mid:
-        return mid(torch, pfb, noise, dev, inflight=args.inflight, pipeline=bool(args.pipeline))
+        return mid(torch, pfb, noise, dev, reps=args.reps, inflight=args.inflight, pipeline=bool(args.pipeline),
+                   graph=bool(args.graph))
     if args.only_twostage:
         return twostage(torch, pfb, noise, args.reps)
     # ---- C2' (4/3) round trip
@@ -182,7 +184,7 @@ def cpu_baselines(pfb):
         "2^22 samples (2 synthesis blocks)")
 
 
-def mid(torch, pfb, noise, dev, reps=3, inflight=1, pipeline=False):
+def mid(torch, pfb, noise, dev, reps=3, inflight=1, pipeline=False, graph=False):
     tm = pfb.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
     nm = 1 << 26
     xm = noise(1, nm)
@@ -195,14 +197,16 @@ def mid(torch, pfb, noise, dev, reps=3, inflight=1, pipeline=False):
         chm = torch.empty((1, Km, 4096), dtype=torch.complex64, device=dev)
         om = torch.empty((1, synm.output_length(Km)), dtype=torch.complex64, device=dev)
         pairs.append((anam, synm, chm, om))
+    # each unit in flight reads its own input (no shared input lines between the units)
+    xs = [xm] + [noise(1, nm) for _ in pairs[1:]]
     if len(pairs) == 1:
         anam, synm, chm, om = pairs[0]
         ms = timeit(torch, lambda: pfb.roundtrip(anam, synm, xm, chan=chm, out=om), reps)
     elif pipeline:
         # the split round trip as a two-stream pipeline (bench.py --pipeline): unit i's
         # FIR + row FFT on stream A beside unit i-1's synthesis on stream S
-        for a, s_, c, o in pairs:
-            pfb.roundtrip(a, s_, xm, chan=c, out=o)
+        for (a, s_, c, o), xi in zip(pairs, xs):
+            pfb.roundtrip(a, s_, xi, chan=c, out=o)
         torch.cuda.synchronize()
         D = len(pairs)
 
@@ -216,7 +220,7 @@ def mid(torch, pfb, noise, dev, reps=3, inflight=1, pipeline=False):
                 a, s_, c, o = pairs[i % D]
                 if i >= D:
                     sa.wait_event(ev_s[i - D])
-                pfb.roundtrip_analysis(a, s_, xm, chan=c)
+                pfb.roundtrip_analysis(a, s_, xs[i % D], chan=c)
                 ev_a[i].record(sa)
                 ss.wait_event(ev_a[i])
                 with torch.cuda.stream(ss):
@@ -227,9 +231,21 @@ def mid(torch, pfb, noise, dev, reps=3, inflight=1, pipeline=False):
         n_it = reps * D
         enqueue(D)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        enqueue(n_it)
-        torch.cuda.synchronize()
+        if graph:
+            # the n_it steps captured as one graph (bench.py's form; eager launches of these
+            # persistent kernels on two streams interleave destructively)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                enqueue(n_it)
+            g.replay()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            g.replay()
+            torch.cuda.synchronize()
+        else:
+            t0 = time.perf_counter()
+            enqueue(n_it)
+            torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / n_it
     else:
         # D units in flight: unit i on plan pair i mod D and stream i mod D (no dependence
@@ -258,7 +274,7 @@ def mid(torch, pfb, noise, dev, reps=3, inflight=1, pipeline=False):
         ms = (time.perf_counter() - t0) * 1e3 / n_it
     emit("roundtrip C3 SKA-Mid padded 4096ch", ms, 16 * (1 + 8 / 7) * nm,
          msamples_per_s=round(nm / ms / 1e3, 1), n_taps=len(tm), units_in_flight=len(pairs),
-         pipeline=bool(pipeline and len(pairs) > 1))
+         pipeline=bool(pipeline and len(pairs) > 1), graph=bool(graph and pipeline and len(pairs) > 1))
 
 
 if __name__ == "__main__":

@@ -33,8 +33,9 @@ import numpy as np
 from .config import as_rational, config_dir, default_config
 from .firio import design_PFB_FIR_filter, design_PFB_FIR_filter_two_stage, read_fir_filter_coeff
 
-__all__ = ["PureTone", "Impulse", "FrequencyComb", "TestPureTone", "TestImpulse",
-           "TestFrequencyComb", "comb_harmonics", "sgcht", "sgcht_config", "header_template"]
+__all__ = ["PureTone", "Impulse", "FrequencyComb", "SquareWave", "FrequencyWedge", "TestPureTone",
+           "TestImpulse", "TestFrequencyComb", "comb_harmonics", "sgcht", "sgcht_config",
+           "sgcht_filename", "header_template", "num2str"]
 
 
 # ------------------------------------------------------------------ generators
@@ -121,6 +122,68 @@ def comb_harmonics(n_chan=1, two_stage=False, invert=False, comb="", nharmonic=3
             fmin += 1.0 / (nch * 4)
             fmax += 1.0 / (nch * 4)
     return amplitudes, np.linspace(fmin, fmax, nharmonic)
+
+
+class SquareWave:
+    """SquareWave.m:1-64: complex Gaussian noise of variance on_amp for the first
+    floor(period duty_cycle) samples of every period, off_amp for the rest (zeros when the
+    amplitude is 0); single precision, the phase carried across calls."""
+
+    def __init__(self, period=26, duty_cycle=0.5, on_amp=1.0, off_amp=0.0, seed=0):
+        self.period = int(period)
+        self.duty_cycle = duty_cycle
+        self.on_amp = on_amp
+        self.off_amp = off_amp
+        self.current = 0
+        self._rng = np.random.default_rng(seed)
+
+    def generate(self, nsample: int):
+        ioff = int(math.floor(self.period * self.duty_cycle))
+        x = np.zeros(nsample, dtype=np.complex64)
+        nout = 0
+        while nout < nsample:  # SquareWave.m:29-56
+            iphase = self.current % self.period
+            if iphase < ioff:
+                n, a = ioff - iphase, math.sqrt(self.on_amp * 0.5)
+            else:
+                n, a = self.period - iphase, math.sqrt(self.off_amp * 0.5)
+            n = min(n, nsample - nout)
+            if a > 0:
+                x[nout:nout + n] = (np.float32(a) * (self._rng.standard_normal(n, dtype=np.float32)
+                                                     + 1j * self._rng.standard_normal(n, dtype=np.float32))
+                                    ).astype(np.complex64)
+            nout += n
+            self.current += n
+        return self, x[None, None, :]
+
+
+class FrequencyWedge:
+    """FrequencyWedge.m:1-66: blocks of ``resolution`` samples of complex noise whose
+    spectrum has the amplitude slope sqrt(fftshift(linspace(0, 1, resolution))), i.e.
+    ifft(slope .* (randn + i randn)) in single precision, streamed across calls."""
+
+    def __init__(self, resolution=1024 * 1024, seed=0):
+        self.resolution = int(resolution)
+        self.slope = np.sqrt(np.fft.fftshift(np.linspace(0.0, 1.0, self.resolution))).astype(np.float32)
+        self.current = 0
+        self.buffer = None
+        self._rng = np.random.default_rng(seed)
+
+    def generate(self, nsample: int):
+        x = np.zeros(nsample, dtype=np.complex64)
+        nout = 0
+        while nout < nsample:
+            if self.current == 0:
+                spec = (self._rng.standard_normal(self.resolution, dtype=np.float32)
+                        + 1j * self._rng.standard_normal(self.resolution, dtype=np.float32))
+                self.buffer = np.fft.ifft((self.slope * spec).astype(np.complex64)).astype(np.complex64)
+            n = min(self.resolution - self.current, nsample - nout)
+            x[nout:nout + n] = self.buffer[self.current:self.current + n]
+            nout += n
+            self.current += n
+            if self.current == self.resolution:
+                self.current = 0
+        return self, x[None, None, :]
 
 
 # ------------------------------------------------------------------ testers
@@ -286,26 +349,92 @@ def sgcht_config(cfg: str):
     return c
 
 
-def sgcht(signal="complex_sinusoid", cfg="", two_stage=False, invert=False, critical=False,
-          combine=1, test=True, blocks=None, blocksz=None, device=0, collect=False,
-          noise=1e-6, seed=0, comb=""):
-    """sgcht.m with ``test=true``: returns a namespace with ``result`` (0 pass, -1 fail, as
-    sgcht returns), ``blocks`` (blocks processed), ``tester`` (the tester object, its
-    ``last`` diagnostics), ``config`` and, with ``collect``, ``outputs`` (the blocks the
-    tester saw, device tensors) and ``inputs`` (the generated host blocks).
+def num2str(x) -> str:
+    """Matlab num2str of a scalar: integers as %d, otherwise %.{max(ceil(log10|x|), 1) + 4}g."""
+    xf = float(x)
+    if xf == int(xf) and abs(xf) < 1e15:
+        return str(int(xf))
+    digits = max(math.ceil(math.log10(abs(xf))), 1) + 4
+    return f"{xf:.{digits}g}"
 
-    Signals: complex_sinusoid (TestPureTone), temporal_impulse (TestImpulse) and
-    frequency_comb (TestFrequencyComb; ``comb`` '', 'coarse' or 'fine', sgcht.m:394-432).
-    sgcht.m:439 assigns ``tester.os_factor = os_factor``, a name sgcht never defines (Matlab
-    would stop there for any comb test with a cfg); the configuration's os_factor — the
-    evident intent — is used.
 
-    Block size / count default to sgcht.m:480-495 (64 Ki samples x 2048 blocks single
+def sgcht_filename(signal, cfg="", cfg2="", comb="", two_stage=False, critical=False, invert=False,
+                   f_taper="", combine=1, single=False, nbit=32, rndInput=False, rmsInput=0.0,
+                   rndOutput=False, rmsOutput=0.0, directory="products"):
+    """sgcht.m:101-163: the output file name, built from the options in the same order."""
+    name = str(signal)
+    if comb in ("coarse", "fine"):
+        name += "_" + comb
+    if cfg:
+        name += "_" + cfg
+    if cfg2:
+        name += "_" + cfg2
+    if two_stage:
+        name += "_two_stage"
+    if critical:
+        name += "_critical"
+    if invert:
+        name += "_inverted"
+    if f_taper:
+        name += "_" + f_taper
+    if combine > 1:
+        name += "_" + str(int(combine))
+    if single:
+        name += "_single"
+    if nbit != 32:
+        name += "_" + str(int(nbit)) + "bit"
+    rndIn = rndInput or rmsInput > 0.0
+    if rndIn:
+        name += "_rndIn"
+    if rmsInput > 0.0:
+        name += "_rmsIn=" + num2str(rmsInput)
+    rndOut = rndOutput or rmsOutput > 0.0
+    if rndOut:
+        name += "_rndOut"
+    if rmsOutput > 0.0:
+        name += "_rmsOut=" + num2str(rmsOutput)
+    return os.path.join(directory, name + ".dada")
+
+
+def sgcht(signal="square_wave", cfg="", two_stage=False, invert=False, critical=False,
+          combine=1, test=False, blocks=None, blocksz=None, device=0, collect=False,
+          noise=1e-6, seed=0, comb="", single=False, f_taper="", nbit=32, scale=1.0,
+          output_nchan=0, periods=0, rndInput=False, rmsInput=0.0, rndOutput=False,
+          rmsOutput=0.0, output_dir=None):
+    """sgcht.m: signal generator -> channeliser -> (inverse) -> tester or DADA file.
+
+    Returns a namespace with ``result`` (0 pass, -1 fail, as sgcht returns), ``blocks``
+    (blocks processed), ``tester`` (its ``last`` diagnostics), ``config``, ``header`` (the
+    output DADA header, sgcht.m:314-356), ``filename`` and, with ``collect``, ``outputs``
+    (the blocks after the channeliser / inverse, device tensors) and ``inputs`` (the
+    generated host blocks).
+
+    test=True (sgcht.m:442-459): complex_sinusoid (TestPureTone), temporal_impulse
+    (TestImpulse) and frequency_comb (TestFrequencyComb; ``comb`` '', 'coarse' or 'fine',
+    sgcht.m:394-432).  sgcht.m:439 assigns ``tester.os_factor = os_factor``, a name sgcht
+    never defines (Matlab would stop there for any comb test with a cfg); the
+    configuration's os_factor — the evident intent — is used.
+
+    test=False (sgcht.m:540-575): each block is scaled by ``scale``, cast to ``nbit``
+    (32: complex single; 16 / 8: Matlab's round-half-away, saturating cast, through
+    pfb_dada_pack), cut to ``output_nchan`` channels and appended to the DADA file
+    ``sgcht_filename(...)`` in ``output_dir`` — written only when ``output_dir`` is given
+    (Matlab always writes ../products/<name>.dada; here a caller that only wants the blocks
+    passes ``collect``).  Signals: square_wave (SquareWave.m, period from the header's
+    CALFREQ, ``periods`` blocks of one period when set), frequency_wedge, frequency_comb,
+    complex_sinusoid, temporal_impulse.  The header gets NBIT, TSAMP (scaled by the
+    channelisation levels), PFB_DC_CHAN, NSTAGE, NCHAN_PFB_0, PFB_NCHAN, OS_FACTOR and the
+    FIR (add_fir_filter_to_header.m, which resets NSTAGE to the number of filters, 1).
+
+    Block size / count default to sgcht.m:480-500 (64 Ki samples x 2048 blocks single
     stage, 128 blocks for the comb, 64 Mi x 2 two-stage, doubled for 'mid'); tests pass
     smaller counts."""
-    if signal not in ("complex_sinusoid", "temporal_impulse", "frequency_comb"):
-        raise ValueError(f"sgcht: testing is implemented for complex_sinusoid, "
-                         f"temporal_impulse and frequency_comb, not {signal!r}")
+    signals = ("square_wave", "frequency_wedge", "frequency_comb", "complex_sinusoid",
+               "temporal_impulse")
+    if signal not in signals:
+        raise ValueError(f"Unrecognized signal: {signal}")
+    if test and signal in ("square_wave", "frequency_wedge"):
+        raise ValueError(f"Testing not implemented for {signal}")  # sgcht.m:376,385
     if comb and (not cfg or signal != "frequency_comb"):  # sgcht.m:106-114
         raise ValueError("Cannot specify comb spacing without analysis filterbank cfg "
                          "and a frequency_comb signal")
@@ -319,36 +448,80 @@ def sgcht(signal="complex_sinusoid", cfg="", two_stage=False, invert=False, crit
         raise ValueError("Cannot invert without analysis filterbank cfg")
     if combine > 1 and not (two_stage and invert):
         raise ValueError("Cannot combine coarse channels without inverting a two-stage bank")
+    if single and not two_stage:
+        raise ValueError("Single-channel output implemented only for two-stage")
     header = header_template(signal)
     tsamp = float(header["TSAMP"])
+    rndIn = rndInput or rmsInput > 0.0
+    rndOut = rndOutput or rmsOutput > 0.0
     config = None
     filterbank = inverse = None
     n_chan = 1
     if cfg:
         config = sgcht_config(cfg)
+        config.rndInput, config.rmsInput = rndIn, rmsInput
+        config.rndOutput, config.rmsOutput = rndOut, rmsOutput
         n_chan = config.channels
+        os1 = config.os_factor
         if two_stage:
             filterbank = TwoStageFilterBank(config, device=device)
             filterbank.critical = int(bool(critical))
+            filterbank.single = int(bool(single))
+            level = 2
         else:
             filterbank = FilterBank(config, device=device)
+            level = 1
         pfb_nchan = n_chan
-        if critical and two_stage:
-            pfb_nchan = config.os_factor.normalize(n_chan)
+        if critical and level == 2:
+            pfb_nchan = os1.normalize(n_chan)
         if invert:
             if two_stage:
                 inverse = TwoStageInverseFilterBank(config, device=device)
+                inverse.single = int(bool(single))
                 inverse.combine = combine
                 inverse.nch2 = int(pfb_nchan)
             else:
                 inverse = InverseFilterBank(config, device=device)
+            if f_taper:
+                inverse = inverse.frequency_taper(f_taper)
+            level -= 1
+        if level != 0:  # sgcht.m:314-356
+            def norm(v):  # normalize.m in double: (de * v) / nu
+                return (os1.de * v) / os1.nu
+            new_tsamp = tsamp
+            if critical and level == 1:
+                new_tsamp = new_tsamp * n_chan
+            else:
+                new_tsamp = norm(new_tsamp) * n_chan
+                if level == 2:
+                    new_tsamp = norm(new_tsamp) * n_chan
+            new_tsamp = new_tsamp / combine
+            header["NBIT"] = num2str(nbit)
+            header["TSAMP"] = num2str(new_tsamp)
+            header["PFB_DC_CHAN"] = "1"
+            header["NSTAGE"] = num2str(level)
+            header["NCHAN_PFB_0"] = num2str(n_chan)
+            if getattr(config, "kept_channels", 0):
+                pfb_nchan = config.kept_channels
+            header["PFB_NCHAN"] = num2str(float(pfb_nchan))
+            header["OS_FACTOR"] = f"{os1.nu}/{os1.de}"
+            from .dada import add_fir_filter_to_header
+            header = add_fir_filter_to_header(header, [config.filt_coeff], [os1])
     if blocksz is None:
         blocksz = 64 * 1024 * 1024 if two_stage else 64 * 1024
         if cfg == "mid":
             blocksz *= 2
     if blocks is None:
         blocks = 2 if two_stage else (128 if signal == "frequency_comb" else 2 * 1024)
-    if signal == "frequency_comb":
+    tester = None
+    if signal == "square_wave":
+        calfreq = float(header["CALFREQ"])  # Hz
+        gen = SquareWave(period=round(1e6 / (calfreq * tsamp)), seed=seed)
+        if periods > 0:
+            blocks, blocksz = int(periods), gen.period  # sgcht.m:497-500
+    elif signal == "frequency_wedge":
+        gen = FrequencyWedge(seed=seed)
+    elif signal == "frequency_comb":
         amps, freqs = comb_harmonics(n_chan, two_stage, invert, comb)
         gen = FrequencyComb(amps, freqs)
         tester = TestFrequencyComb(freqs)
@@ -367,29 +540,48 @@ def sgcht(signal="complex_sinusoid", cfg="", two_stage=False, invert=False, crit
             fir_offset = config.fir_offset_direction * (taps // 2)
             filter_offset = output_overlap - 1 + config.kludge_offset
         tester = TestImpulse(offset=int(gen.offset + fir_offset - filter_offset))
+    filename = sgcht_filename(signal, cfg, "", comb, two_stage, critical, invert, f_taper, combine,
+                              single, nbit, rndInput, rmsInput, rndOutput, rmsOutput,
+                              directory=output_dir or "products")
     res = SimpleNamespace(result=0, blocks=0, tester=tester, config=config, n_chan=n_chan,
+                          header=header, filename=filename if (output_dir and not test) else None,
                           outputs=[] if collect else None, inputs=[] if collect else None)
+    writer = None
+    if output_dir and not test:
+        from .dada import DADAWrite
+        os.makedirs(output_dir, exist_ok=True)
+        writer = DADAWrite(filename, header, nbit=nbit).open(filename)
     torch = None
-    if filterbank is not None:
+    if filterbank is not None or writer is not None:
         import torch
-    for _ in range(int(blocks)):  # sgcht.m:504-575
-        gen, x = gen.generate(int(blocksz))
-        if x.shape[-1] == 0:
-            break
-        if collect:
-            res.inputs.append(x)
-        if torch is not None:  # one copy of the block to the device; it stays there
-            x = torch.from_numpy(x).to(torch.device("cuda", int(device)))
-        if filterbank is not None:
-            filterbank, x = filterbank.execute(x)
-        if inverse is not None:
-            inverse, x = inverse.execute(x)
-        if collect:
-            res.outputs.append(x)
-        res.blocks += 1
-        if test:
-            tester, r = tester.test(x)
-            if r != 0:
-                res.result = -1
-                return res
+    try:
+        for _ in range(int(blocks)):  # sgcht.m:504-575
+            gen, x = gen.generate(int(blocksz))
+            if x.shape[-1] == 0:
+                break
+            if collect:
+                res.inputs.append(x)
+            if torch is not None:  # one copy of the block to the device; it stays there
+                x = torch.from_numpy(x).to(torch.device("cuda", int(device)))
+            if filterbank is not None:
+                filterbank, x = filterbank.execute(x)
+            if inverse is not None:
+                inverse, x = inverse.execute(x)
+            if collect:
+                res.outputs.append(x)
+            res.blocks += 1
+            if test:
+                tester, r = tester.test(x)
+                if r != 0:
+                    res.result = -1
+                    return res
+            elif writer is not None:
+                if scale != 1:
+                    x = scale * x
+                if output_nchan > 0:
+                    x = x[:, :output_nchan, :]
+                writer.write(x)
+    finally:
+        if writer is not None:
+            writer.close()
     return res

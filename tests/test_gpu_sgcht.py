@@ -215,3 +215,48 @@ def test_sgcht_frequency_comb_tester_agrees_with_oracle_chain(gpu, case):
     assert got == want, f"device verdicts {got} != oracle chain verdicts {want}"
     if inv and not two:
         assert all(r == 0 for r in got), got
+
+
+@pytest.mark.parametrize("signal,cfg,kw", [
+    ("square_wave", "low", {}),
+    ("frequency_wedge", "low", {"nbit": 16, "scale": 100.0}),
+    ("square_wave", "low", {"invert": True}),
+    ("complex_sinusoid", "low", {"output_nchan": 64}),
+])
+def test_sgcht_write_mode_dada_file(gpu, tmp_path, signal, cfg, kw):
+    """sgcht(test=false) writes the channelised (or inverted) blocks to a DADA file
+    (sgcht.m:540-575, DADAWrite.m): the header has the level-scaled TSAMP, NSTAGE (reset to
+    1 by add_fir_filter_to_header.m), NCHAN_PFB_0, PFB_NCHAN, OS_FACTOR and the FIR; the
+    data section read back (read_dada_file) equals the blocks — scaled, cast to NBIT with
+    Matlab's round-half-away saturating cast, cut to output_nchan."""
+    import torch
+    pfb = _pfb()
+    res = pfb.sgcht(signal=signal, cfg=cfg, blocks=4, blocksz=1 << 16, collect=True,
+                    output_dir=str(tmp_path), seed=3, **kw)
+    assert res.filename and res.filename.startswith(str(tmp_path))
+    data, hdr = pfb.dada.read_dada_file(res.filename)
+    got = data.cpu().numpy()
+    parts = []
+    for y in res.outputs:
+        v = y if hasattr(y, "cpu") else torch.from_numpy(np.asarray(y)).to(gpu)
+        v = v.cpu().numpy().astype(np.complex128) * kw.get("scale", 1.0)
+        if kw.get("output_nchan"):
+            v = v[:, :kw["output_nchan"], :]
+        parts.append(v)
+    want = np.concatenate(parts, axis=2)
+    nbit = kw.get("nbit", 32)
+    if nbit != 32:
+        want = (orc.matlab_round(want.real) + 1j * orc.matlab_round(want.imag))
+        lim = 2 ** (nbit - 1)
+        want = np.clip(want.real, -lim, lim - 1) + 1j * np.clip(want.imag, -lim, lim - 1)
+    assert got.shape == want.shape
+    assert np.array_equal(got, want.astype(np.complex64)), float(np.abs(got - want).max())
+    inv = kw.get("invert", False)
+    assert hdr["NBIT"] == str(nbit) and hdr["NCHAN"] == str(got.shape[1])
+    if not inv:  # one analysis level: TSAMP x (7/8 or 3/4) x n_chan
+        assert hdr["NSTAGE"] == "1" and hdr["NCHAN_PFB_0"] == "256" and hdr["OS_FACTOR"] == "4/3"
+        t0 = float(pfb.streaming.header_template(signal)["TSAMP"])
+        assert float(hdr["TSAMP"]) == pytest.approx(t0 * 3 / 4 * 256, rel=1e-4)
+        assert hdr["PFB_NCHAN"] == "256" and hdr["NTAP_0"] == str(len(res.config.filt_coeff))
+    else:  # level 0: sgcht.m leaves the header as the template has it
+        assert "NSTAGE" not in hdr and hdr["TSAMP"] == pfb.streaming.header_template(signal)["TSAMP"]
