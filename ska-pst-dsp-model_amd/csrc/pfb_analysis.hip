@@ -774,9 +774,11 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
     // round trip: the channelised rows come from the Z rows (already in output-row order,
     // N^2 x the FIR sums, index-reversed for the padded variant): the same row FFT on
     // the same values scaled by 2^k, so the result is bit-identical to the scratch path
-    if (a.row0 != 0 || a.z_row0 != 0 || (a.variant == kPadded && !a.zrev)) return hipErrorInvalidValue;
-    RowFftArgs rz{a.z, a.z_pol_stride, a.out, a.out_pol_stride, rows, a.zrev, nullptr, a.twN,
-                  1.0f / (float)a.N, 0, 0, 0, a.K_total};
+    // (z_stage 2 on rows [row0, K): Z rows are output rows, so both sides start at row0)
+    if ((a.row0 != 0 && a.z_stage != 2) || a.z_row0 != 0 || (a.variant == kPadded && !a.zrev))
+      return hipErrorInvalidValue;
+    RowFftArgs rz{a.z + a.row0 * a.N, a.z_pol_stride, a.out + a.row0 * a.N, a.out_pol_stride, rows, a.zrev,
+                  nullptr, a.twN, 1.0f / (float)a.N, 0, 0, 0, a.K_total};
     if (a.variant == kBunton) return dispatch_row_fft<-1>(a.N, rz, a.n_pol, s);
     return dispatch_row_fft<+1>(a.N, rz, a.n_pol, s);
   }

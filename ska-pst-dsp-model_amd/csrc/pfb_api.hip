@@ -1572,6 +1572,40 @@ static pfb_status roundtrip_run(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, c
       HIPCHK(hipStreamWaitEvent(s, pa->events[1], 0));
       return PFB_OK;
     }
+    // generic (N > 256) path in chunks of synthesis blocks (PFB_RT_C3_CHUNKS=n, experiments
+    // A/B): FIR -> row FFT -> synthesis per chunk, so each chunk's stage-1 rows are read by
+    // the row FFT and the synthesis shortly after the FIR wrote them (Infinity-Cache
+    // resident, profiles/r04_v1_mall_probe.jsonl).  Z row t comes from FIR row
+    // (t + sds) mod K (padded circular shift), so the rows of Z [z_lo, z_hi) are FIR rows
+    // [z_lo + sds, z_hi + sds), the part past K wrapping to [0, ...).
+    static const int c3_chunks = pfb::knob("PFB_RT_C3_CHUNKS") ? std::atoi(pfb::knob("PFB_RT_C3_CHUNKS")) : 0;
+    if (!pa->fused && c3_chunks > 1 && z0 == 0 && !zblk && B >= c3_chunks) {
+      const int64_t sds = pa->variant == pfb::kPadded ? pa->sds : 0;
+      int64_t zdone = 0;
+      for (int64_t c = 0; c < c3_chunks; ++c) {
+        const int64_t b0 = B * c / c3_chunks, b1 = B * (c + 1) / c3_chunks;
+        const int64_t need = (c == c3_chunks - 1) ? K : std::min(K, off + b1 * ps->keep + 2 * (int64_t)ps->Ov);
+        if (need > zdone) {
+          const int64_t k0 = zdone + sds, k1 = need + sds;
+          pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, std::min(k0, K), std::min(k1, K), K, s, Z,
+                                       zrows * pa->N, 0, 0, nullptr, 0, nullptr, 1);
+          if (st != PFB_OK) return st;
+          if (k1 > K) {  // the wrapped tail of Z: FIR rows [max(k0 - K, 0), k1 - K)
+            st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, std::max<int64_t>(k0 - K, 0), k1 - K, K, s, Z,
+                              zrows * pa->N, 0, 0, nullptr, 0, nullptr, 1);
+            if (st != PFB_OK) return st;
+          }
+          st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, zdone, need, K, s, Z, zrows * pa->N, 0, 0, nullptr,
+                            0, nullptr, 2);
+          if (st != PFB_OK) return st;
+          zdone = need;
+        }
+        pfb_status st = synthesis_blocks(ps, Z + (off + b0 * ps->keep) * pa->N, zrows * pa->N, b0, b1 - b0,
+                                         (float2*)out, out_ps, olen, s, 0);
+        if (st != PFB_OK) return st;
+      }
+      return PFB_OK;
+    }
     if (C <= 1 || !zblk) {
       pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0,
                                    nullptr, zblk);
