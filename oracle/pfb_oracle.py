@@ -618,8 +618,19 @@ class FilterBankOracle:
         self.filt_coeff = np.asarray(filt_coeff, dtype=np.float64).ravel()
         self.n_chan = int(n_chan)
         self.os_factor = _os(os_factor)
-        self.pfb_analysis = {"polyphase_analysis": polyphase_analysis,
-                             "polyphase_analysis_padded": polyphase_analysis_padded}[analysis]
+        if analysis == "polyphase_analysis_lowcbf":
+            # polyphase_analysis_lowcbf.m:27-34: `persistent do_padding` — the 1536 leading
+            # zeros on the first call of the session only (one object = one session here)
+            self._lowcbf_first = True
+
+            def _lowcbf(x, filt, n_chan, os_factor):
+                y = polyphase_analysis_lowcbf(x, filt, do_padding=self._lowcbf_first)
+                self._lowcbf_first = False
+                return y
+            self.pfb_analysis = _lowcbf
+        else:
+            self.pfb_analysis = {"polyphase_analysis": polyphase_analysis,
+                                 "polyphase_analysis_padded": polyphase_analysis_padded}[analysis]
         self.rndInput, self.rmsInput = rndInput, rmsInput
         self.rndOutput, self.rmsOutput = rndOutput, rmsOutput
         self.input_buffer = None

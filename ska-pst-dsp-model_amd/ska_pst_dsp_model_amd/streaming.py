@@ -340,7 +340,9 @@ def sgcht_config(cfg: str):
         c.filt_coeff = read_fir_filter_coeff(c.fir_filter_path)
     else:
         d = getattr(c, "fir_design", {"kind": "single_stage", "taps_per_chan": 12})
-        if d["kind"] == "two_stage":
+        if d["kind"] == "file":  # a stand-in tap file of the package's config directory
+            c.filt_coeff = read_fir_filter_coeff(os.path.join(config_dir, d["path"]))
+        elif d["kind"] == "two_stage":
             c.filt_coeff = design_PFB_FIR_filter_two_stage(c.channels, c.os_factor, d["taps_per_chan"])
         else:
             c.filt_coeff = design_PFB_FIR_filter(c.channels, c.os_factor, d["taps_per_chan"])

@@ -4,6 +4,7 @@ and the harness' naming helpers.  No device needed."""
 import io
 
 import numpy as np
+import pytest
 
 from oracle import pfb_oracle as orc
 
@@ -305,3 +306,25 @@ def test_sgcht_filename_and_header_without_gpu():
         "p/square_wave_low_two_stage_critical_inverted_16_8bit.dada"
     assert sg.sgcht_filename("frequency_comb", "mid", comb="coarse", rmsOutput=2.5) == \
         "products/frequency_comb_coarse_mid_rndOut_rmsOut=2.5.dada"
+
+
+@pytest.mark.parametrize("name,N,os_,func", [
+    ("sps", 256, "32/27", "polyphase_analysis"),
+    ("lowpsi", 256, "4/3", "polyphase_analysis_lowcbf"),
+    ("lowpsi_old", 256, "4/3", "polyphase_analysis_lowcbf"),
+    ("low_alt", 256, "4/3", "polyphase_analysis"),
+    ("low", 256, "4/3", "polyphase_analysis"),
+    ("mid", 4096, "8/7", "polyphase_analysis_padded"),
+    ("low_external", 256, "4/3", "polyphase_analysis"),
+    ("mid_external", 4096, "8/7", "polyphase_analysis_padded"),
+])
+def test_every_reference_sub_config_loads(name, N, os_, func):
+    """Every sub-config of the reference's config/test.config.json (default_config.m /
+    load_config) exists here with its analysis function, channels and OS factor, and
+    sgcht_config attaches taps (the tap file, else the documented stand-in)."""
+    from ska_pst_dsp_model_amd import streaming as sg
+    c = sg.sgcht_config(name)
+    assert c.channels == N and str(c.os_factor) == os_ and c.analysis_function == func
+    assert len(c.filt_coeff) > 0
+    if func == "polyphase_analysis_lowcbf":
+        assert len(c.filt_coeff) == 3072

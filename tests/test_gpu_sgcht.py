@@ -107,6 +107,17 @@ CHAIN_CASES = [
     ("mid", "temporal_impulse", False, False, False, 1, 8, 1 << 17),
     ("mid", "complex_sinusoid", False, True, False, 1, 32, 1 << 17),
     ("mid", "temporal_impulse", False, True, False, 1, 32, 1 << 17),
+    # the reference's other sub-configs (config/test.config.json): 'sps' (OS 32/27, P 24:
+    # the fused analysis kernel, W = 216 synthesis), 'low_external' (P 11, off the
+    # streaming kernel), 'lowpsi' (the LowCBF PST filterbank through FilterBank, one-time
+    # pre-padding on the first chunk, 216 channels)
+    ("sps", "complex_sinusoid", False, False, False, 1, 8, 1 << 16),
+    ("sps", "complex_sinusoid", False, True, False, 1, 16, 1 << 16),
+    ("sps", "temporal_impulse", False, True, False, 1, 16, 1 << 16),
+    ("low_external", "complex_sinusoid", False, True, False, 1, 16, 1 << 16),
+    ("low_external", "temporal_impulse", False, True, False, 1, 16, 1 << 16),
+    ("lowpsi", "complex_sinusoid", False, False, False, 1, 8, 1 << 16),
+    ("lowpsi", "temporal_impulse", False, False, False, 1, 8, 1 << 16),
     # (the frequency comb's chains: COMB_CASES below)
 ]
 
