@@ -1035,12 +1035,9 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
   p->L = W * N;
   p->Lov = (int)(((int64_t)Ov * de * N) / nu);
   p->Lkeep = p->L - 2 * p->Lov;
-  // L_ov = Ov*de/nu*N is a multiple of N when Ov*de/nu is integral; the block kernel
-  // emits y[t0 + N t1] for t1 in [t1_lo, t1_hi)
-  if (p->Lov % N != 0) {
-    delete p;
-    return fail(PFB_ERR_UNSUPPORTED, "output_overlap not a multiple of n_chan");
-  }
+  // the kernels keep y[t0 + N t1] when L_ov <= t0 + N t1 < L - L_ov (sample-exact: L_ov =
+  // Ov de/nu N need not be a multiple of N — normalize(os, Ov) = 40.5 for the reference's
+  // 'sps' config); [t1_lo, t1_hi) bounds the t1 that hold any kept sample
   p->t1_lo = p->Lov / N;
   p->t1_hi = W - p->t1_lo;
   p->deripple = d->apply_deripple != 0;

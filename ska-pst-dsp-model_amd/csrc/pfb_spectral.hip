@@ -105,7 +105,9 @@ struct WOutStore {
     if (r >= n_rows || t1 < t1_lo || t1 >= t1_hi) return;
     const int64_t b = r / N;
     const int t0 = (int)(r - b * N);
-    const int64_t idx = (blk0 + b) * Lkeep + t0 + (int64_t)N * t1 - Lov;
+    const int64_t rel = t0 + (int64_t)N * t1 - Lov;  // kept position (L_ov need not be a multiple of N)
+    if (rel < 0 || rel >= Lkeep) return;
+    const int64_t idx = (blk0 + b) * Lkeep + rel;
     if (idx >= out_limit) return;
     if (spans) {
       double s, c;

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(NTPW) __attribute__((amdgpu_waves_per_eu(2))) void 
     const int64_t nk =
         (tmask(a.timing_mask) & 2) ? 0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
     return PairOut<P16>{make_rsrc(opol + ob, (uint32_t)nk * 8u),
-                   make_rsrc(opol + ob + 1, (uint32_t)max((int64_t)0, nk - 1) * 8u), N, a.t1_lo, t0,
+                   make_rsrc(opol + ob + 1, (uint32_t)max((int64_t)0, nk - 1) * 8u), N, a.Lov, t0,
                    a.scale};
   };
 
@@ -159,7 +159,7 @@ static hipError_t launch_sb(const SynthBlockArgs& a, hipStream_t s) {
     constexpr int DK = synth_reuse_dk<NF, W>();
     constexpr bool FU = SynthPlan<NF, W>::fused;
     const bool reuse = DK > 0 && a.keep == DK * NB1 && !a.no_reuse;
-    const bool p16 = (a.out_limit % 2 == 0) && (a.Lkeep % 2 == 0);
+    const bool p16 = (a.out_limit % 2 == 0) && (a.Lkeep % 2 == 0) && (a.Lov % 2 == 0);
     // table copy in LDS where it still leaves 4 two-wave workgroups per CU (the VGPR
     // limit): SKA-Mid 25.7 + 14 KB; not SKA-Low (38.5 + 28 KB)
     constexpr size_t t4_bytes = (size_t)W * PAIRS * 16;

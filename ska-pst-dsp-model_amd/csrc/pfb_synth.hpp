@@ -105,13 +105,15 @@ struct PairOut {
   // descriptors keep the two 8-byte stores from being merged into one 16-byte store,
   // so each sample is range-checked on its own (the output limit may split a pair).
   __amdgpu_buffer_rsrc_t o, o1;
-  int N, t1_lo, t0;
+  int N, lov, t0;  // lov = L_ov: the block's first kept sample is t0 + N t1 = L_ov
   float scale;
   template <class P, class RR>
   __device__ __forceinline__ void store(int q, int t1, cpx2 v, P, RR) const {
-    // negative offsets (t1 < t1_lo, q = kDropPair) wrap past 2^31 bytes and are dropped
-    // by the range check
-    const int off = ((t1 - t1_lo) * N + t0 + 2 * q) * 8;
+    // sample t0 + 2q + N t1 of the block goes to kept position t0 + 2q + N t1 - L_ov:
+    // negative offsets (the discarded head, q = kDropPair) wrap past 2^31 bytes and are
+    // dropped by the range check, as is the discarded tail past L_keep (L_ov need not be a
+    // multiple of N: normalize(os, Ov) may be fractional, e.g. 48 x 27/32 for 'sps')
+    const int off = (t1 * N - lov + t0 + 2 * q) * 8;
     const Interleaved y = to_interleaved(cscale(v, scale));
     if constexpr (P16) {
       // (t0 + 2q even, nk even): a pair never straddles the range end, so the 16-byte

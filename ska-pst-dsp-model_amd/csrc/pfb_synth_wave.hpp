@@ -332,7 +332,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       const __amdgpu_buffer_rsrc_t o = make_rsrc(opol + ob, (uint32_t)nk * 8u);
       // lanes t1a >= RW hold no output: their offsets leave the descriptor's range (as do
       // the discarded t1 < t1_lo, whose negative offsets wrap past 2^31)
-      int base = (t1a < RW) ? ((t1a - a.t1_lo) * N + t0g + col2) * 8 : (int)0x80000000;
+      int base = (t1a < RW) ? (t1a * N - a.Lov + t0g + col2) * 8 : (int)0x80000000;
       // (FIR variant: recomputed every block — 16 hoisted store offsets would spill)
       if constexpr (FIRV::kOn) asm volatile("" : "+v"(base));
       static_for<0, 16>([&](auto t) {

@@ -249,7 +249,7 @@ void synth_wave512_kernel(SynthBlockArgs a) {
       const __amdgpu_buffer_rsrc_t o = make_rsrc(opol + ob, (uint32_t)nk * 8u);
       // lanes t1a >= 28 hold no output: their offsets leave the descriptor's range (as do
       // the discarded t1 < t1_lo, whose negative offsets wrap past 2^31)
-      int base = (t1a < 28) ? ((t1a - a.t1_lo) * N + t0g + col2) * 8 : (int)0x80000000;
+      int base = (t1a < 28) ? (t1a * N - a.Lov + t0g + col2) * 8 : (int)0x80000000;
       // (recomputed every block: 16 hoisted store offsets would not fit the register budget)
       asm volatile("" : "+v"(base));
       static_for<0, 16>([&](auto t) {

@@ -564,3 +564,26 @@ def test_inverse_filterbank_frequency_taper_stream(gpu):
         assert got.shape == ref.shape
         if ref.size:
             assert_pfb_close(got, ref, what=f"inverse filterbank hann n={n}")
+
+
+@pytest.mark.parametrize("N,os_,nf,ov,spans", [
+    (256, "32/27", 256, 48, 1),   # 'sps': normalize(os, Ov) = 40.5 -> L_ov = 10368 = 40.5 N
+    (8, "32/27", 128, 16, 1),     # L_ov = 108 = 13.5 N (the pair-store block kernel)
+    (8, "8/7", 128, 7, 0),        # L_ov = 49: odd (single-sample stores), critical
+])
+def test_synthesis_fractional_output_overlap(gpu, N, os_, nf, ov, spans):
+    """output_overlap = normalize(os, Ov) * n_chan (polyphase_synthesis.m:117) need not be a
+    multiple of n_chan: the kept samples iFFFF(output_overlap + 1 : L - output_overlap)
+    (:302) then start mid-way through a t1 row.  The kernels discard sample-exactly
+    (offset t0 + N t1 - L_ov, range-checked)."""
+    import torch
+    pfb = _pfb()
+    tpc = 24 if os_ == "32/27" and N == 256 else 10
+    taps = pfb.design_PFB_FIR_filter(N, os_, tpc)
+    x = _noise(np.random.default_rng(61), (2, N, (nf - 2 * ov) * 7 + 2 * ov + 5))
+    dr = {"apply_deripple": 1, "filter_coeff": taps}
+    win = orc.pfb_window("tukey", nf, ov)
+    ref = orc.polyphase_synthesis(x, spans, nf, os_, dr, 1, ov, win)
+    got = pfb.polyphase_synthesis(torch.from_numpy(x).to(gpu), spans, nf, os_, dr, 1, ov,
+                                  pfb.PFBWindow().lookup["tukey"](nf, ov))
+    assert_pfb_close(got.cpu().numpy(), ref, what=f"synthesis {N} ch {os_} Ov {ov}")
