@@ -71,9 +71,7 @@ __global__ __launch_bounds__(NTPW) __attribute__((amdgpu_waves_per_eu(2))) void 
     const int64_t avail = a.out_limit - ob;
     const int64_t nk =
         (tmask(a.timing_mask) & 2) ? 0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
-    return PairOut<P16>{make_rsrc(opol + ob, (uint32_t)nk * 8u),
-                   make_rsrc(opol + ob + 1, (uint32_t)max((int64_t)0, nk - 1) * 8u), N, a.Lov, t0,
-                   a.scale};
+    return PairOut<P16>{make_rsrc(opol + ob, (uint32_t)nk * 8u), N, a.Lov, t0, a.scale};
   };
 
   if constexpr (!SP::fused) {

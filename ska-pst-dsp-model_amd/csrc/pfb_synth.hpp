@@ -100,11 +100,13 @@ struct PairSelect {
 template <bool P16>
 struct PairOut {
   static constexpr bool kIsLds = false;
-  // o: first kept output sample of the block, records = kept samples in bytes;
-  // o1: the same shifted by one sample (the odd phase of each pair).  Separate
-  // descriptors keep the two 8-byte stores from being merged into one 16-byte store,
-  // so each sample is range-checked on its own (the output limit may split a pair).
-  __amdgpu_buffer_rsrc_t o, o1;
+  // o: first kept output sample of the block, records = kept samples in bytes.  Without
+  // P16 each sample of a pair is range-checked on its own (the output limit or an odd L_ov
+  // may split a pair): the odd sample's offset is hidden from the optimiser so the two
+  // 8-byte stores are never merged into one 16-byte store.  (It must be off + 8 on o, not
+  // off on a descriptor based one sample later: at kept position 0 that offset is -8,
+  // which the range check drops.)
+  __amdgpu_buffer_rsrc_t o;
   int N, lov, t0;  // lov = L_ov: the block's first kept sample is t0 + N t1 = L_ov
   float scale;
   template <class P, class RR>
@@ -121,8 +123,10 @@ struct PairOut {
       __builtin_amdgcn_raw_buffer_store_b128(
           __builtin_bit_cast(v4u, v4f{y.lo.x, y.lo.y, y.hi.x, y.hi.y}), o, off, 0, 0);
     } else {
+      int off1 = off + 8;
+      asm volatile("" : "+v"(off1));
       __builtin_amdgcn_raw_buffer_store_b64(as_u(y.lo), o, off, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b64(as_u(y.hi), o1, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(as_u(y.hi), o, off1, 0, 0);
     }
   }
 };

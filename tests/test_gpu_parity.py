@@ -568,7 +568,7 @@ def test_inverse_filterbank_frequency_taper_stream(gpu):
 
 @pytest.mark.parametrize("N,os_,nf,ov,spans", [
     (256, "32/27", 256, 48, 1),   # 'sps': normalize(os, Ov) = 40.5 -> L_ov = 10368 = 40.5 N
-    (8, "32/27", 128, 16, 1),     # L_ov = 108 = 13.5 N (the pair-store block kernel)
+    (8, "32/27", 256, 16, 1),     # L_ov = 108 = 13.5 N (the pair-store block kernel)
     (8, "8/7", 128, 7, 0),        # L_ov = 49: odd (single-sample stores), critical
 ])
 def test_synthesis_fractional_output_overlap(gpu, N, os_, nf, ov, spans):
