@@ -37,22 +37,25 @@ def main():
     taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
     g = torch.Generator(device=dev).manual_seed(100)
     n = 1 << 24
-    x = (torch.complex(torch.randn((args.n_pol, n), device=dev, generator=g),
-                       torch.randn((args.n_pol, n), device=dev, generator=g)) / np.sqrt(2)).to(torch.complex64)
+
+    def noise():
+        return (torch.complex(torch.randn((args.n_pol, n), device=dev, generator=g),
+                              torch.randn((args.n_pol, n), device=dev, generator=g)) / np.sqrt(2)).to(torch.complex64)
     win = pfb.PFBWindow().lookup["tukey"](256, 48)
     D = max(1, args.inflight)
     graphs, streams = [], [torch.cuda.Stream(dev) for _ in range(D)]
     keep = []  # the plans and buffers each captured graph writes stay alive while it replays
     for _ in range(D):
+        x = noise()  # distinct inputs per pair, as bench.py's units (none stays cache-resident)
         ana = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", args.n_pol, 0)
         syn = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, args.n_pol, 0)
         K = ana.output_length(n)
         chan = torch.empty((args.n_pol, K, 256), dtype=torch.complex64, device=dev)
         out = torch.empty((args.n_pol, syn.output_length(K)), dtype=torch.complex64, device=dev)
 
-        keep.append((ana, syn, chan, out))
+        keep.append((ana, syn, chan, out, x))
 
-        def step(ana=ana, syn=syn, chan=chan, out=out):
+        def step(ana=ana, syn=syn, chan=chan, out=out, x=x):
             pfb.roundtrip(ana, syn, x, chan=chan, out=out)
         for _ in range(2):
             step()

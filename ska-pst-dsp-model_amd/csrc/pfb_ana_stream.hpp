@@ -94,7 +94,7 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
   // last row instead: an L2 hit rather than HBM traffic nobody uses
   const int r_last = (int)(st1 - st0 - 1) * NEW + WIN - 1;
   auto ld = [&](int r) {  // window row r (relative to row_first)
-    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (uint32_t)((min(r, r_last) * N + c + shift) * 8), 0, 0);
+    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (uint32_t)((min(r, r_last) * N + c + shift) * 8), 0, kAuxIn);
     return __builtin_bit_cast(v2f, v);
   };
   // (re, im) as a packed pair: one v_pk_fma_f32 per complex x real tap MAC
@@ -186,7 +186,8 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
           constexpr float n2 = (float)N * (float)N;
           const v2f a0 = acc[s - 1][qq] * n2, a1 = acc[s][qq] * n2;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{a0.x, a0.y, a1.x, a1.y}), zb,
-                                                 (uint32_t)((((r0 / ZOUT) * N + c) * ZOUT + r0 % ZOUT) * 8), 0, 0);
+                                                 (uint32_t)((((r0 / ZOUT) * N + c) * ZOUT + r0 % ZOUT) * 8), 0,
+                                                 kAuxZst);
         }
       });
     });

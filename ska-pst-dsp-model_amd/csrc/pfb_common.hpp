@@ -16,6 +16,42 @@ namespace pfb {
 
 constexpr int NT = 256;  // threads per workgroup (4 wave64)
 
+// Cache policy (the buffer instructions' aux operand; gfx950: 1 = sc0, 2 = nt, 16 = sc1) of
+// the C2 round trip's streams: analysis input loads, channelised-row stores, stage-1 row
+// stores and loads, synthesis output stores.  Compile-time; a variant library is built with
+// -DPFB_AUX_*=... (scripts/gpu_aux_ab.sh).  Measured (cache-policy A/B):
+// nontemporal stores of the two products nobody re-reads (channelised rows, synthesis
+// output) 1.5-2.7 % faster per pipelined step; nt on the stage-1 rows (re-read by the
+// synthesis while partly Infinity-Cache resident) or on the input loads is slower.
+#ifndef PFB_AUX_IN
+#define PFB_AUX_IN 0
+#endif
+#ifndef PFB_AUX_CHAN
+#define PFB_AUX_CHAN 2
+#endif
+#ifndef PFB_AUX_ZST
+#define PFB_AUX_ZST 0
+#endif
+#ifndef PFB_AUX_ZLD
+#define PFB_AUX_ZLD 0
+#endif
+#ifndef PFB_AUX_OUT
+#define PFB_AUX_OUT 2
+#endif
+// the same for the C3 (SKA-Mid) kernels' streams: FIR stage-1 row stores, row-FFT
+// (RowStore) stores, synth_wave512 output stores (1 = nontemporal: the C3 round trip 1.9 %
+// faster; its 613 MB of stage-1 rows exceed the Infinity Cache anyway)
+#ifndef PFB_NT_C3
+#define PFB_NT_C3 1
+#endif
+constexpr bool kNtC3 = PFB_NT_C3 != 0;
+__device__ __forceinline__ void st_c3(float2* p, float2 v) {
+  if constexpr (kNtC3) __builtin_nontemporal_store(__builtin_bit_cast(v2f, v), reinterpret_cast<v2f*>(p));
+  else *p = v;
+}
+constexpr int kAuxIn = PFB_AUX_IN, kAuxChan = PFB_AUX_CHAN, kAuxZst = PFB_AUX_ZST, kAuxZld = PFB_AUX_ZLD,
+              kAuxOut = PFB_AUX_OUT;
+
 // ======================================================================= functors
 struct AnalysisStore {
   static constexpr bool kIsLds = false;
@@ -50,7 +86,7 @@ struct BufRowStore {
   float scale;
   __device__ __forceinline__ void store(int row, int c, float2 v) const {
     const uint32_t off = row >= lo ? (uint32_t)((row * N + c) * 8) : 0xFFFFFFF0u;
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v, scale)), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v, scale)), r, off, 0, kAuxChan);
   }
   // rows [k0, k0 + T) of a [row][N] array at `base`, valid rows [k_lo, k_hi)
   __device__ __forceinline__ static BufRowStore rows(float2* base, int64_t k0, int T, int64_t k_lo,
@@ -153,7 +189,7 @@ struct RowStore {
         t -= sds;
         while (t < 0) t += n_total;
       }
-      out[t * N + c] = cscale(v, scale);
+      st_c3(out + t * N + c, cscale(v, scale));
     }
   }
 };

@@ -84,7 +84,7 @@ struct FirShape {
 // round trip measured and rejected in round 3)
 struct RangeSched {
   static constexpr bool kReuse = true;
-  static constexpr int kLoadAux = 0;
+  static constexpr int kLoadAux = kAuxZld;
   int b_begin, n;
   __device__ int count() const { return n; }
   __device__ int block(int i) const { return b_begin + i; }
@@ -337,7 +337,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       if constexpr (FIRV::kOn) asm volatile("" : "+v"(base));
       static_for<0, 16>([&](auto t) {
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v[t]), o,
-                                              (uint32_t)(base + t * RW * N * 8), 0, 0);
+                                              (uint32_t)(base + t * RW * N * 8), 0, kAuxOut);
       });
     }
     if constexpr (FIRV::kOn) {
