@@ -742,6 +742,7 @@ struct pfb_synthesis_plan {
   int no_reuse = 0;  // PFB_SYNTH_NO_REUSE: re-read the overlap rows (A/B measurement only)
   int xcd = 1;       // PFB_SYNTH_XCD=0: plain workgroup order (A/B measurement only)
   bool identity_perm = true;
+  bool win_flat = false;  // SynthBlockArgs::win_flat
   bool has_cgain = false;
   bool has_spectral = false;  // non-identity spectral taper: pfb_spectral.hip path
   DevBuf window, tw4, tw4s, twN, twNf, twW, perm, cgain;
@@ -908,6 +909,7 @@ static pfb::SynthBlockArgs synth_args(const pfb_synthesis_plan* p, const float2*
   a.t1_hi = p->t1_hi;
   a.scale = (float)((double)p->de / (double)p->nu / (double)p->L);
   a.window = p->window.as<float>();
+  a.win_flat = p->win_flat ? 1 : 0;
   a.spans = p->spans;
   a.tw4 = p->tw4.as<float2>();
   a.tw4s = p->tw4s.as<float2>();
@@ -1137,6 +1139,10 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
     expo[(size_t)jp] = e;
     gain[(size_t)jp] = (j < W2) ? g[(size_t)(W2 - j)] : g[(size_t)(j - W2)];
   }
+  // the rows the wave synthesis kernels treat as flat: [48, 208) at Nf 256, [128, 384) at 512
+  p->win_flat = (Nf == 256 || Nf == 512) &&
+                std::all_of(window.begin() + (Nf == 256 ? 48 : 128), window.begin() + (Nf == 256 ? 208 : 384),
+                            [](float w) { return w == 1.f; });
   hipError_t e = upload(p->window, window);
   // four-step twiddle x deripple gain, laid out [j'][t0] (coalesced in the block kernel)
   std::vector<float2> tw4((size_t)N * W), tw4s((size_t)N * W);

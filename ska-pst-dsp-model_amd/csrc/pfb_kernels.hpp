@@ -121,6 +121,8 @@ struct SynthBlockArgs {
   int N, Nf, W, keep, L, Lov, Lkeep, t1_lo, t1_hi;
   float scale;
   const float* window;     // Nf temporal window (device)
+  int win_flat;            // 1: window[t] == 1 exactly for t in [48, 208) at Nf 256 / [128, 384) at
+                           // Nf 512 (the wave kernels skip those taper multiplies)
   int spans;               // 1: spans Nyquist (signed-frequency bins), 0: critical
   const float2* tw4;       // [j'][t0] = gain[j'] e^{+2 pi i t0 expo[j'] / L} (W x N)
   const float2* twNf;      // e^{-2 pi i m / Nf}

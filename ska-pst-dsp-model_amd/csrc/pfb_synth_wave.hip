@@ -49,9 +49,9 @@ bool synth_wave_fir_supported(const SynthBlockArgs& a) {
   return (a.fir_n_dat + 512 * (int64_t)a.N) * 8 < kRsrcMaxBytes;
 }
 
-template <int RW, bool SPANS, bool XW, class FIRV = NoFir>
+template <int RW, bool SPANS, bool XW, class FIRV = NoFir, bool WFLAT = false>
 static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
-  auto kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV>;
+  auto kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT>;
   hipError_t e = set_lds(kern, kLdsB);
   if (e != hipSuccess) return e;
   const int groups = a.N / kCols;
@@ -82,6 +82,14 @@ hipError_t launch_synth_wave(const SynthBlockArgs& a, hipStream_t s) {
   // profiles/r03_v8_c2_wave_xw_ab.jsonl); PFB_WAVE_XW=0: within the wave (experiments A/B)
   static const bool xw = !(knob("PFB_WAVE_XW") && std::atoi(knob("PFB_WAVE_XW")) == 0);
   if (!kExperiments || xw) {
+    // a window flat over rows [48, 208) (tukey, Ov <= 48: C2) skips 10 of the 16 taper
+    // multiplies per lane and block (PFB_WAVE_WFLAT=0: the general kernel, experiments A/B)
+    static const bool wf_off = knob("PFB_WAVE_WFLAT") && std::atoi(knob("PFB_WAVE_WFLAT")) == 0;
+    if (a.win_flat && !wf_off) {
+      if (a.W == 224)
+        return a.spans ? launch_wave_t<14, true, true, NoFir, true>(a, s) : launch_wave_t<14, false, true, NoFir, true>(a, s);
+      return a.spans ? launch_wave_t<12, true, true, NoFir, true>(a, s) : launch_wave_t<12, false, true, NoFir, true>(a, s);
+    }
     if (a.W == 224) return a.spans ? launch_wave_t<14, true, true>(a, s) : launch_wave_t<14, false, true>(a, s);
     return a.spans ? launch_wave_t<12, true, true>(a, s) : launch_wave_t<12, false, true>(a, s);
   }

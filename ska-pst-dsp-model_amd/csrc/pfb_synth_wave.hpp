@@ -97,7 +97,10 @@ struct RangeSched {
 // in wave l / 4): one Z load instruction reads 2 row pairs x the 16 phases (256-B runs)
 // instead of 8 row pairs x 4 phases (64-B runs), and swap 1 crosses waves (one more
 // workgroup barrier per block)
-template <int RW, bool SPANS, int DK, class SCHED, bool XW = false, class FIRV = NoFir>
+// WFLAT: the temporal window is exactly 1 on rows [48, 208) of the block (tukey with Ov <= 48,
+// SynthBlockArgs::win_flat): registers r = 3 .. 12 (rows l + 16 r) skip the multiply — the
+// product by 1 is exact, so the output is bit-identical
+template <int RW, bool SPANS, int DK, class SCHED, bool XW = false, class FIRV = NoFir, bool WFLAT = false>
 __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol, int tg, const SCHED& sch) {
   constexpr int W = 16 * RW;
   static_assert(RW <= 14 && RW % 2 == 0, "W = 16 RW with RW even and <= 14");
@@ -266,7 +269,16 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     __syncthreads();
     // ---- pass 1: taper, 16-point DFT over r, twiddle
     float2 v[16];
-    {
+    if constexpr (WFLAT) {
+      const v4f q0 = *reinterpret_cast<const v4f*>(winrow);       // rows l + 16 r, r < 4
+      const v4f q3 = *reinterpret_cast<const v4f*>(winrow + 48);  // r >= 12
+      static_for<0, 16>([&](auto rv) {
+        constexpr int r = decltype(rv)::value;
+        if constexpr (r < 3) v[r] = cscale(x[r], q0[r]);
+        else if constexpr (r > 12) v[r] = cscale(x[r], q3[r - 12]);
+        else v[r] = x[r];
+      });
+    } else {
       float wv[16];
       static_for<0, 4>([&](auto k) {
         const v4f q = *reinterpret_cast<const v4f*>(winrow + 16 * k);
@@ -357,7 +369,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
   }
 }
 
-template <int RW, bool SPANS, int DK, bool XW = false, class FIRV = NoFir>
+template <int RW, bool SPANS, int DK, bool XW = false, class FIRV = NoFir, bool WFLAT = false>
 __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(3)))
 void synth_wave_kernel(SynthBlockArgs a) {
   const int groups = a.N / kCols;
@@ -366,8 +378,8 @@ void synth_wave_kernel(SynthBlockArgs a) {
   const int Rg = gridDim.x / groups;
   const int b_begin = (int)((int64_t)a.n_blocks * rr / Rg);
   const int b_end = (int)((int64_t)a.n_blocks * (rr + 1) / Rg);
-  synth_wave_body<RW, SPANS, DK, RangeSched, XW, FIRV>(a, blockIdx.y, lt % groups,
-                                                       RangeSched{b_begin, b_end - b_begin});
+  synth_wave_body<RW, SPANS, DK, RangeSched, XW, FIRV, WFLAT>(a, blockIdx.y, lt % groups,
+                                                              RangeSched{b_begin, b_end - b_begin});
 }
 
 }  // namespace pfb

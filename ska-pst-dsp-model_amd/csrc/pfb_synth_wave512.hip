@@ -82,7 +82,9 @@ __device__ __forceinline__ void twiddle_rows(float2* v, const char* row) {
 // XW: pass-1 lanes (phase p, FFT lane m) spread over the workgroup (lane = 8 (m mod 8) + p in
 // wave m / 8): one Z load instruction reads 8 rows x the 8 phases (64-B runs) instead of 32
 // rows x 2 phases, and swap 1 crosses waves (one more workgroup barrier per block)
-template <bool SPANS, bool XW>
+// WFLAT: the temporal window is exactly 1 on rows [128, 384) (tukey with Ov <= 128,
+// SynthBlockArgs::win_flat): registers r = 4 .. 11 (rows m + 32 r) skip the multiply (exact)
+template <bool SPANS, bool XW, bool WFLAT = false>
 __global__ __launch_bounds__(kW5Threads) __attribute__((amdgpu_waves_per_eu(3)))
 void synth_wave512_kernel(SynthBlockArgs a) {
   constexpr int W = 448, DK = 8;  // keep = 256 rows = 8 register rows of 32
@@ -190,7 +192,16 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     __syncthreads();
     // ---- pass 1: taper, 16-point DFT over r, x w_512^{m f1}
     float2 v[16];
-    {
+    if constexpr (WFLAT) {
+      const v4f q0 = *reinterpret_cast<const v4f*>(winrow);       // r < 4
+      const v4f q3 = *reinterpret_cast<const v4f*>(winrow + 48);  // r >= 12
+      static_for<0, 16>([&](auto rv) {
+        constexpr int r = decltype(rv)::value;
+        if constexpr (r < 4) v[r] = cscale(x[r], q0[r]);
+        else if constexpr (r >= 12) v[r] = cscale(x[r], q3[r - 12]);
+        else v[r] = x[r];
+      });
+    } else {
       float wv[16];
       static_for<0, 4>([&](auto k) {
         const v4f q = *reinterpret_cast<const v4f*>(winrow + 16 * k);
@@ -266,9 +277,9 @@ bool synth_wave512_supported(const SynthBlockArgs& a) {
          a.N <= 65536 && a.tw4s != nullptr;
 }
 
-template <bool SPANS, bool XW>
+template <bool SPANS, bool XW, bool WFLAT = false>
 static hipError_t launch_w5(const SynthBlockArgs& a, hipStream_t s) {
-  auto kern = synth_wave512_kernel<SPANS, XW>;
+  auto kern = synth_wave512_kernel<SPANS, XW, WFLAT>;
   hipError_t e = set_lds(kern, kW5LdsB);
   if (e != hipSuccess) return e;
   const int groups = a.N / kW5Cols;
@@ -287,6 +298,10 @@ hipError_t launch_synth_wave512(const SynthBlockArgs& a, hipStream_t s) {
   if (!synth_wave512_supported(a)) return hipErrorInvalidValue;
   // (PFB_W5_XW=0: pass-1 lanes inside one wave per phase pair, experiments build A/B)
   static const bool xw = !(knob("PFB_W5_XW") && std::atoi(knob("PFB_W5_XW")) == 0);
+  // (PFB_WAVE_WFLAT=0: the general taper, experiments A/B)
+  static const bool wf_off = knob("PFB_WAVE_WFLAT") && std::atoi(knob("PFB_WAVE_WFLAT")) == 0;
+  if (a.win_flat && !wf_off)
+    return a.spans ? launch_w5<true, true, true>(a, s) : launch_w5<false, true, true>(a, s);
   if (!kExperiments || xw) return a.spans ? launch_w5<true, true>(a, s) : launch_w5<false, true>(a, s);
   return a.spans ? launch_w5<true, false>(a, s) : launch_w5<false, false>(a, s);
 }

@@ -263,6 +263,25 @@ def test_synthesis_nf512_wave_kernel(gpu, N, spans, deripple, taper):
     assert_pfb_close(got, ref, what=f"synthesis Nf 512 N={N} spans={spans} dr={deripple} {taper}")
 
 
+@pytest.mark.parametrize("spans", [1, 0])
+def test_synthesis_nf512_wave_kernel_non_flat_window(gpu, spans):
+    """The wave kernels skip the taper multiply where the window is exactly 1 (rows
+    [128, 384) at Nf 512: tukey, top_hat, no_window); an explicit window that is not runs
+    the general taper — against the oracle with the same coefficients."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(64, "8/7", 12)
+    x = _noise(np.random.default_rng(77 + spans), (2, 64, 7 * 256 + 256 + 11))
+    t = np.arange(512)
+    win = np.asarray(orc.pfb_window("tukey", 512, 128), dtype=np.float64).reshape(-1)
+    win = win * (0.75 + 0.25 * np.cos(2 * np.pi * t / 512))
+    dr = {"apply_deripple": 1, "filter_coeff": taps}
+    ref = orc.polyphase_synthesis(x, spans, 512, "8/7", dr, 3, 128, lambda a, nf, ov: a * win[None, :])
+    got = pfb.polyphase_synthesis(torch.from_numpy(x).cuda(), spans, 512, "8/7", dr, 3, 128,
+                                  pfb.PFBWindow().custom(win))
+    assert_pfb_close(got.cpu().numpy(), ref, what=f"synthesis Nf 512 non-flat window spans={spans}")
+
+
 @pytest.mark.parametrize("taper,combine", [("tukey", 1), ("hann", 1), ("tukey", 2)])
 def test_synthesis_4096_persistent_chan_ifft(gpu, taper, combine):
     """4096-channel synthesis with more than 2048 channelised rows in one chunk: the

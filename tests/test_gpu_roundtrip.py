@@ -92,6 +92,29 @@ def test_roundtrip_matches_separate_calls(gpu, case):
         assert torch.equal(out, out_ref), "synthesised output differs"
 
 
+@pytest.mark.parametrize("os_,n_pol", [("8/7", 1), ("4/3", 2)])
+def test_roundtrip_wave_general_window(gpu, os_, n_pol):
+    """The wave synthesis skips the taper multiply on rows [48, 208) when the window is
+    exactly 1 there (tukey / top_hat / no_window at Ov 48: every other test); a window that
+    is not runs the general taper.  Both against the separate calls (block kernel)."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, os_, 12)
+    x = _noise_t(torch, gpu, (n_pol, 1 << 19), 11)
+    t = np.arange(256)
+    tukey = orc.tukey_window_coeffs(256, 48)
+    for win in (tukey * (0.75 + 0.25 * np.cos(2 * np.pi * t / 256)), tukey):
+        ana = pfb.AnalysisPlan(taps, 256, os_, "polyphase_analysis", n_pol, 0)
+        syn = pfb.SynthesisPlan(256, os_, 256, 48, True, 1, True, taps, pfb.PFBWindow().custom(win),
+                                None, n_pol, 0)
+        out_ref = syn.execute(ana.execute(x), sample_offset=1, layout="ptc")
+        _, out = pfb.roundtrip(ana, syn, x, sample_offset=1)
+        torch.cuda.synchronize()
+        assert out.shape == out_ref.shape and out.shape[1] > 0
+        assert_pfb_close(out.cpu().numpy(), out_ref.cpu().numpy(), scale=1.0,
+                         what=f"wave synthesis, {'tukey' if win is tukey else 'non-flat'} window")
+
+
 def test_roundtrip_no_blocks_only_analysis(gpu):
     """Too short for one synthesis block: the channelised product is still produced."""
     import torch
