@@ -264,7 +264,8 @@ __device__ __forceinline__ void run_rest(const LdsRows& lds, const Last& last, c
 // columns in registers, and loads row r + 1 into registers while it transforms row r.
 // (The one-shot kernel re-read the 32 KB table from L2 for every one of the 73 400 C3
 // rows and waited for each row's loads with nothing in flight.)
-template <int N, int DIR, bool PERM, bool GAIN>
+// PF: rows prefetched ahead (1, or 2 with 32 more VGPRs: 64 KB in flight per workgroup)
+template <int N, int DIR, bool PERM, bool GAIN, int PF = 1>
 __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
   static_assert(RowShape<N>::ROWS == 1, "one row per workgroup");
   constexpr int R = FirstPassOf<N, 1, NT>::R, NB = N / R;
@@ -287,18 +288,23 @@ __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
     col[r] = PERM ? a.perm[i] : i;
     g[r] = GAIN ? a.cgain[col[r]] : 1.f;
   }
-  float2 pf[R];
-  auto load_row = [&](int64_t row) {
+  float2 pf[PF][R];
+  auto load_row = [&](int64_t row, float2* d) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) pf[r] = in[row * N + col[r]];
+    for (int r = 0; r < R; ++r) d[r] = in[row * N + col[r]];
   };
-  load_row(q0);
+#pragma unroll
+  for (int k = 0; k < PF; ++k) load_row(min(q0 + k, q1 - 1), pf[k]);
 #pragma unroll 1
   for (int64_t row = q0; row < q1; ++row) {
     float2 v[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[r] = GAIN ? cscale(pf[r], g[r]) : pf[r];
-    load_row(min(row + 1, q1 - 1));  // unconditional: the last row re-reads itself
+    for (int r = 0; r < R; ++r) v[r] = GAIN ? cscale(pf[0][r], g[r]) : pf[0][r];
+#pragma unroll
+    for (int k = 0; k + 1 < PF; ++k)
+#pragma unroll
+      for (int r = 0; r < R; ++r) pf[k][r] = pf[k + 1][r];
+    load_row(min(row + PF, q1 - 1), pf[PF - 1]);  // unconditional: past the end re-reads the last row
     __syncthreads();  // tables / the previous row's last pass done with the LDS row
     // first pass (radix R, stride 1): no twiddles, outputs j R + r
     sdft<R, DIR>(v);

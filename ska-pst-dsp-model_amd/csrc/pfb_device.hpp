@@ -118,6 +118,14 @@ constexpr int first_factor(int R) {
   return R;
 }
 
+constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+// x^{-1} mod m (gcd(x, m) = 1)
+constexpr int cinv_mod(int x, int m) {
+  for (int i = 1; i < m; ++i)
+    if ((x * i) % m == 1) return i;
+  return m == 1 ? 0 : -1;
+}
+
 // In-place DFT of R points held in registers, natural order in and out.
 // DIR = -1: X[k] = sum x[n] e^{-2 pi i n k / R}; DIR = +1: unnormalised inverse.
 // C is float2 (one transform) or any complex type with the helpers above.
@@ -182,6 +190,30 @@ __device__ __forceinline__ void sdft(C* v) {
       }
     });
     static_for<0, R>([&](auto k) { v[k] = out[k]; });
+  } else if constexpr (cgcd(first_factor(R), R / first_factor(R)) == 1) {
+    // R = A B with A, B coprime (6, 12, 14, 28, ...): Good-Thomas prime-factor mapping, no
+    // twiddles.  Input n = (B n1 + A n2) mod R; X[(B u k1 + A v k2) mod R] = z[k1][k2] with
+    // u = B^{-1} mod A, v = A^{-1} mod B (W_R^{n k} = W_A^{n1 k1} W_B^{n2 k2}: the cross
+    // terms are multiples of R).  Every index is a compile-time register permutation.
+    constexpr int A = first_factor(R);
+    constexpr int B = R / A;
+    constexpr int U = cinv_mod(B % A, A), V = cinv_mod(A % B, B);
+    static_assert(A > 1 && B > 1 && U > 0 && V > 0, "prime-factor split");
+    C y[A][B];
+    static_for<0, A>([&](auto n1) {
+      static_for<0, B>([&](auto n2) {
+        y[n1][n2] = v[(B * decltype(n1)::value + A * decltype(n2)::value) % R];
+      });
+      sdft<B, DIR>(y[n1]);
+    });
+    static_for<0, B>([&](auto k2) {
+      C z[A];
+      static_for<0, A>([&](auto n1) { z[n1] = y[n1][k2]; });
+      sdft<A, DIR>(z);
+      static_for<0, A>([&](auto k1) {
+        v[(B * U * decltype(k1)::value + A * V * decltype(k2)::value) % R] = z[k1];
+      });
+    });
   } else {
     constexpr int A = first_factor(R);
     constexpr int B = R / A;

@@ -23,7 +23,12 @@ static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s
     static const int env_wgs = knob("PFB_ROWFFT_WGS") ? std::atoi(knob("PFB_ROWFFT_WGS")) : 0;
     if (env_wgs > 0) wgs = env_wgs;
     if (!off && r.n_rows >= 4 * wgs) {
-      auto kern = row_fft_persist_kernel<N, DIR, PERM, GAIN>;
+      // (PFB_ROWFFT_PF=2: two rows prefetched ahead, experiments A/B)
+      auto kern = row_fft_persist_kernel<N, DIR, PERM, GAIN, 1>;
+      if constexpr (kExperiments) {
+        static const bool pf2 = knob("PFB_ROWFFT_PF") && std::atoi(knob("PFB_ROWFFT_PF")) == 2;
+        if (pf2) kern = row_fft_persist_kernel<N, DIR, PERM, GAIN, 2>;
+      }
       hipError_t e = set_lds(kern, bytes);
       if (e != hipSuccess) return e;
       dim3 grid((unsigned)std::max<int64_t>(1, wgs / n_pol), (unsigned)n_pol);

@@ -65,13 +65,26 @@ static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
   return launch_kernel(kern, grid, dim3(kWgThreads), kLdsB, s, a);
 }
 
+// the flat-window choice of the stored-rows kernel (PFB_WAVE_WFLAT=0: off, experiments A/B)
+static bool use_wflat(const SynthBlockArgs& a) {
+  static const bool wf_off = knob("PFB_WAVE_WFLAT") && std::atoi(knob("PFB_WAVE_WFLAT")) == 0;
+  return a.win_flat && !wf_off;
+}
+
+template <int RW, int NU, int DE, bool WFLAT>
+static hipError_t launch_wave_fir_w(const SynthBlockArgs& a, hipStream_t s) {
+  if (a.fir_pe == 14)
+    return a.spans ? launch_wave_t<RW, true, false, FirShape<NU, DE, 14>, WFLAT>(a, s)
+                   : launch_wave_t<RW, false, false, FirShape<NU, DE, 14>, WFLAT>(a, s);
+  return a.spans ? launch_wave_t<RW, true, false, FirShape<NU, DE, 13>, WFLAT>(a, s)
+                 : launch_wave_t<RW, false, false, FirShape<NU, DE, 13>, WFLAT>(a, s);
+}
+// (the same taper form as the stored-rows kernel: with a flat window the products by 1 are
+// dropped in both, so the compiler fuses the same multiplies into the same FMAs and the
+// outputs stay bit-identical)
 template <int RW, int NU, int DE>
 static hipError_t launch_wave_fir(const SynthBlockArgs& a, hipStream_t s) {
-  if (a.fir_pe == 14)
-    return a.spans ? launch_wave_t<RW, true, false, FirShape<NU, DE, 14>>(a, s)
-                   : launch_wave_t<RW, false, false, FirShape<NU, DE, 14>>(a, s);
-  return a.spans ? launch_wave_t<RW, true, false, FirShape<NU, DE, 13>>(a, s)
-                 : launch_wave_t<RW, false, false, FirShape<NU, DE, 13>>(a, s);
+  return use_wflat(a) ? launch_wave_fir_w<RW, NU, DE, true>(a, s) : launch_wave_fir_w<RW, NU, DE, false>(a, s);
 }
 
 hipError_t launch_synth_wave(const SynthBlockArgs& a, hipStream_t s) {
@@ -84,8 +97,7 @@ hipError_t launch_synth_wave(const SynthBlockArgs& a, hipStream_t s) {
   if (!kExperiments || xw) {
     // a window flat over rows [48, 208) (tukey, Ov <= 48: C2) skips 10 of the 16 taper
     // multiplies per lane and block (PFB_WAVE_WFLAT=0: the general kernel, experiments A/B)
-    static const bool wf_off = knob("PFB_WAVE_WFLAT") && std::atoi(knob("PFB_WAVE_WFLAT")) == 0;
-    if (a.win_flat && !wf_off) {
+    if (use_wflat(a)) {
       if (a.W == 224)
         return a.spans ? launch_wave_t<14, true, true, NoFir, true>(a, s) : launch_wave_t<14, false, true, NoFir, true>(a, s);
       return a.spans ? launch_wave_t<12, true, true, NoFir, true>(a, s) : launch_wave_t<12, false, true, NoFir, true>(a, s);

@@ -273,7 +273,7 @@ def test_synthesis_nf512_wave_kernel_non_flat_window(gpu, spans):
     taps = pfb.design_PFB_FIR_filter(64, "8/7", 12)
     x = _noise(np.random.default_rng(77 + spans), (2, 64, 7 * 256 + 256 + 11))
     t = np.arange(512)
-    win = np.asarray(orc.pfb_window("tukey", 512, 128), dtype=np.float64).reshape(-1)
+    win = orc.tukey_window_coeffs(512, 128)
     win = win * (0.75 + 0.25 * np.cos(2 * np.pi * t / 512))
     dr = {"apply_deripple": 1, "filter_coeff": taps}
     ref = orc.polyphase_synthesis(x, spans, 512, "8/7", dr, 3, 128, lambda a, nf, ov: a * win[None, :])
