@@ -366,7 +366,9 @@ struct FirLdsShape {
   static constexpr int CWP = CW + 1;                       // padded ring row (banks)
 };
 
-template <int PW, int DE, int NU, int VARIANT>
+// PFD: iterations of input rows held in registers ahead of the ring (1, or 2: twice the
+// bytes in flight per workgroup, experiments A/B PFB_FIR_PF=2)
+template <int PW, int DE, int NU, int VARIANT, int PFD = 1>
 __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges, int cs, int xcd) {
   using SH = FirLdsShape<NU, DE>;
   constexpr int CW = SH::CW, U = SH::U, RR = SH::RR, CWP = SH::CWP, NPF = SH::NPF, MIR = SH::MIR;
@@ -442,15 +444,16 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges,
     const int64_t rho = (int64_t)DE * (qw - 1) + e_min + 1 + i / CW;
     ring_put(rho, i % CW, ld(rho, (c0 + i % CW + cs) % N));
   }
-  v2f pf[NPF];
-  auto prefetch = [&](int64_t qi) {  // rows (DE (qi - 1) + e_max, DE (qi - 1) + e_max + U DE]
+  v2f pf[PFD][NPF];
+  auto prefetch = [&](int64_t qi, v2f* d) {  // rows (DE (qi - 1) + e_max, DE (qi - 1) + e_max + U DE]
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {
       const int i = min(tid + j * NT, SH::BATCH - 1);
-      pf[j] = ld((int64_t)DE * (qi - 1) + e_max + 1 + i / CW, (c0 + i % CW + cs) % N);
+      d[j] = ld((int64_t)DE * (qi - 1) + e_max + 1 + i / CW, (c0 + i % CW + cs) % N);
     }
   };
-  prefetch(qw);
+#pragma unroll
+  for (int k = 0; k < PFD; ++k) prefetch(qw + k * U, pf[k]);
 
   // outputs: Z rows (round trip) or scratch rows at channel position pos
   const int pos = VARIANT == kBunton ? c : N - 1 - c;
@@ -483,10 +486,14 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges,
       const int i = tid + j * NT;
       if (i < SH::BATCH) {
         const int64_t rho = (int64_t)DE * (qi - 1) + e_max + 1 + i / CW;
-        ring_put(rho, i % CW, pf[j]);
+        ring_put(rho, i % CW, pf[0][j]);
       }
     }
-    prefetch(qi + U);
+#pragma unroll
+    for (int k = 0; k + 1 < PFD; ++k)
+#pragma unroll
+      for (int j = 0; j < NPF; ++j) pf[k][j] = pf[k + 1][j];
+    prefetch(qi + PFD * U, pf[PFD - 1]);
     __syncthreads();
     // this iteration's rows DE qi + e - DE + 1 + [0, U DE): one base, immediate offsets
     const v2f* rb = ring + (int)(((int64_t)DE * qi + e - DE + 1) & (RR - 1)) * CWP + cl;
@@ -526,7 +533,7 @@ static hipError_t launch_fir_lds_t(const AnalysisArgs& a, hipStream_t s) {
   }();
   int64_t ranges = std::max<int64_t>(1, std::min<int64_t>(target / chunks, nq / (4 * SH::U)));
   // one range reads rows [DE (q0 - NJ) + e_min - DE, DE q1 + e_max + 2 U DE]: within a descriptor
-  const int64_t halo_rows = PW + 3 * DE + 2 * SH::U * DE + 2 * NU + 4;
+  const int64_t halo_rows = PW + 3 * DE + 3 * SH::U * DE + 2 * NU + 4;  // (3 U DE: PFD <= 2)
   const int64_t fit_rows = kRsrcMaxBytes / 8 / a.N - halo_rows;
   if (fit_rows <= 0) return hipErrorInvalidValue;
   ranges = std::max(ranges, (nq * DE + fit_rows - 1) / fit_rows);
@@ -537,6 +544,16 @@ static hipError_t launch_fir_lds_t(const AnalysisArgs& a, hipStream_t s) {
   static const bool no_zalign = knob("PFB_FIR_ZALIGN") && std::atoi(knob("PFB_FIR_ZALIGN")) == 0;
   const int cs = (a.variant == kPadded && a.z && !no_zalign) ? a.N - 1 : 0;
   static const int xcd = knob("PFB_FIR_LDS_XCD") ? std::atoi(knob("PFB_FIR_LDS_XCD")) : 1;
+  if constexpr (kExperiments) {
+    static const bool pf2 = knob("PFB_FIR_PF") && std::atoi(knob("PFB_FIR_PF")) == 2;
+    if (pf2) {
+      if (a.variant == kBunton)
+        hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kBunton, 2>), grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);
+      else
+        hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kPadded, 2>), grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);
+      return hipGetLastError();
+    }
+  }
   if (a.variant == kBunton)
     hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kBunton>), grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);
   else
