@@ -214,11 +214,13 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
           const float2 v0 = cscale(cm.load(r0, ch), (float)N), v1 = cscale(cm.load(r0 + 1, ch), (float)N);
           const uint32_t off = (uint32_t)((ch * a.out_cs + r0) * 8);
           if (r0 >= lo && r0 + 1 < hi) {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{v0.x, v0.y, v1.x, v1.y}), r, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{v0.x, v0.y, v1.x, v1.y}), r, off, 0,
+                                                   kAuxColMajor);
           } else {
-            if (r0 >= lo && r0 < hi) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v0), r, off, 0, 0);
+            if (r0 >= lo && r0 < hi)
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v0), r, off, 0, kAuxColMajor);
             if (r0 + 1 >= lo && r0 + 1 < hi)
-              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v1), r, off + 8, 0, 0);
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v1), r, off + 8, 0, kAuxColMajor);
           }
         });
       } else {

@@ -38,6 +38,18 @@ constexpr int NT = 256;  // threads per workgroup (4 wave64)
 #ifndef PFB_AUX_OUT
 #define PFB_AUX_OUT 2
 #endif
+// strided channelised rows (a two-stage cascade's assembled stage-2 output): nt, the
+// cascade 0.200-0.203 -> 0.192-0.195 ms (profiles/r04_v7_twostage_cache_policy_ab.jsonl);
+// nt on the channel-major stage-1 product that stage 2 reads next: no consistent change
+#ifndef PFB_AUX_STRIDED
+#define PFB_AUX_STRIDED 2
+#endif
+constexpr int kAuxStrided = PFB_AUX_STRIDED;
+// channel-major channelised rows (a cascade's stage-1 product, read by stage 2 next)
+#ifndef PFB_AUX_COLMAJOR
+#define PFB_AUX_COLMAJOR 0
+#endif
+constexpr int kAuxColMajor = PFB_AUX_COLMAJOR;
 // the same for the C3 (SKA-Mid) kernels' streams: FIR stage-1 row stores, row-FFT
 // (RowStore) stores, synth_wave512 output stores (1 = nontemporal: the C3 round trip 1.9 %
 // faster; its 613 MB of stage-1 rows exceed the Infinity Cache anyway)
@@ -116,7 +128,7 @@ struct StridedRowStore {
       ok = ok && (c < split || c >= split + shift) && j < nsel;
     }
     const uint32_t off = ok ? (uint32_t)((row * rs + j * cs) * 8) : 0xFFFFFFF0u;
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v, scale)), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v, scale)), r, off, 0, kAuxStrided);
   }
   // the host checks that (T rs + jn cs) * 8 fits one descriptor (pfb_api.hip)
   __device__ __forceinline__ static StridedRowStore rows(float2* base, int64_t k0, int T, int64_t k_lo,
