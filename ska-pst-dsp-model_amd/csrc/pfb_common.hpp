@@ -50,6 +50,11 @@ constexpr int kAuxStrided = PFB_AUX_STRIDED;
 #define PFB_AUX_COLMAJOR 0
 #endif
 constexpr int kAuxColMajor = PFB_AUX_COLMAJOR;
+// LowCBF (PST filterbank) output rows: a product, as the channelised rows
+#ifndef PFB_AUX_LCBF
+#define PFB_AUX_LCBF PFB_AUX_CHAN
+#endif
+constexpr int kAuxLcbf = PFB_AUX_LCBF;
 // the same for the C3 (SKA-Mid) kernels' streams: FIR stage-1 row stores, row-FFT
 // (RowStore) stores, synth_wave512 output stores (1 = nontemporal: the C3 round trip 1.9 %
 // faster; its 613 MB of stage-1 rows exceed the Infinity Cache anyway)
@@ -154,7 +159,7 @@ struct LcbfRowStore {
   __device__ __forceinline__ void store(int row, int f, float2 v) const {
     const int c = (f + 108) & 255;
     const uint32_t off = (row >= lo && c < 216) ? (uint32_t)((row * 216 + c) * 8) : 0xFFFFFFF0u;
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v, scale)), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v, scale)), r, off, 0, kAuxLcbf);
   }
   __device__ __forceinline__ static LcbfRowStore rows(float2* base, int64_t k0, int T, int64_t k_lo,
                                                        int64_t k_hi, float scale) {

@@ -121,12 +121,12 @@ struct PairOut {
       // (t0 + 2q even, nk even): a pair never straddles the range end, so the 16-byte
       // store is dropped or kept as a whole exactly when its two samples are
       __builtin_amdgcn_raw_buffer_store_b128(
-          __builtin_bit_cast(v4u, v4f{y.lo.x, y.lo.y, y.hi.x, y.hi.y}), o, off, 0, 0);
+          __builtin_bit_cast(v4u, v4f{y.lo.x, y.lo.y, y.hi.x, y.hi.y}), o, off, 0, kAuxOut);
     } else {
       int off1 = off + 8;
       asm volatile("" : "+v"(off1));
-      __builtin_amdgcn_raw_buffer_store_b64(as_u(y.lo), o, off, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b64(as_u(y.hi), o, off1, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(as_u(y.lo), o, off, 0, kAuxOut);
+      __builtin_amdgcn_raw_buffer_store_b64(as_u(y.hi), o, off1, 0, kAuxOut);
     }
   }
 };
