@@ -259,7 +259,7 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
         t = k - a.sds;
         while (t < 0) t += a.K_total;
       }
-      if (t >= a.z_row0) st_c3(zc + (t - a.z_row0) * N, make_float2(zscale * acc.x, zscale * acc.y));
+      if (t >= a.z_row0) st_nt<kNtFirZ>(zc + (t - a.z_row0) * N, make_float2(zscale * acc.x, zscale * acc.y));
     }
   };
   if constexpr (U > 1) {
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges,
         t = k - a.sds;
         while (t < 0) t += a.K_total;  // once, unless the series is shorter than sds rows
       }
-      if (t >= a.z_row0) zc[(t - a.z_row0) * N] = make_float2(zscale * acc.x, zscale * acc.y);
+      if (t >= a.z_row0) st_nt<kNtFirZ>(zc + (t - a.z_row0) * N, make_float2(zscale * acc.x, zscale * acc.y));
     }
   };
 

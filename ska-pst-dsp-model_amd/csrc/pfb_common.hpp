@@ -55,15 +55,27 @@ constexpr int kAuxColMajor = PFB_AUX_COLMAJOR;
 #define PFB_AUX_LCBF PFB_AUX_CHAN
 #endif
 constexpr int kAuxLcbf = PFB_AUX_LCBF;
-// the same for the C3 (SKA-Mid) kernels' streams: FIR stage-1 row stores, row-FFT
-// (RowStore) stores, synth_wave512 output stores (1 = nontemporal: the C3 round trip 1.9 %
-// faster; its 613 MB of stage-1 rows exceed the Infinity Cache anyway)
-#ifndef PFB_NT_C3
-#define PFB_NT_C3 1
+// the same for the C3 (SKA-Mid, N > 256) kernels' streams, nontemporal (1) or default (0):
+// the FIR's stage-1 rows (PFB_NT_FIRZ), the row FFT's rows (RowStore, PFB_NT_ROW), the
+// synth_wave512 output (PFB_NT_W5).  Measured: the C3 round trip 0.960/0.967 -> 0.936/0.954
+// ms with ROW + W5 (profiles/r04_v5_cache_policy_ab.jsonl); per stream
+// (profiles/r04_v9_c3_cache_policy_ab.jsonl, two boxes): all three nt 0.960-0.968 / 0.955-
+// 0.961 against 0.974-0.988 / 0.961-0.972 with the FIR rows at the default policy — the
+// 613 MB of rows exceed the Infinity Cache, and the row FFT that reads them runs 258-261
+// instead of 282-289 us
+#ifndef PFB_NT_FIRZ
+#define PFB_NT_FIRZ 1
 #endif
-constexpr bool kNtC3 = PFB_NT_C3 != 0;
-__device__ __forceinline__ void st_c3(float2* p, float2 v) {
-  if constexpr (kNtC3) __builtin_nontemporal_store(__builtin_bit_cast(v2f, v), reinterpret_cast<v2f*>(p));
+#ifndef PFB_NT_ROW
+#define PFB_NT_ROW 1
+#endif
+#ifndef PFB_NT_W5
+#define PFB_NT_W5 1
+#endif
+constexpr bool kNtFirZ = PFB_NT_FIRZ != 0, kNtRow = PFB_NT_ROW != 0, kNtW5 = PFB_NT_W5 != 0;
+template <bool NT>
+__device__ __forceinline__ void st_nt(float2* p, float2 v) {
+  if constexpr (NT) __builtin_nontemporal_store(__builtin_bit_cast(v2f, v), reinterpret_cast<v2f*>(p));
   else *p = v;
 }
 constexpr int kAuxIn = PFB_AUX_IN, kAuxChan = PFB_AUX_CHAN, kAuxZst = PFB_AUX_ZST, kAuxZld = PFB_AUX_ZLD,
@@ -206,7 +218,7 @@ struct RowStore {
         t -= sds;
         while (t < 0) t += n_total;
       }
-      st_c3(out + t * N + c, cscale(v, scale));
+      st_nt<kNtRow>(out + t * N + c, cscale(v, scale));
     }
   }
 };

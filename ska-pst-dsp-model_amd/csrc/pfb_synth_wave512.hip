@@ -265,7 +265,7 @@ void synth_wave512_kernel(SynthBlockArgs a) {
       asm volatile("" : "+v"(base));
       static_for<0, 16>([&](auto t) {
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v[t]), o,
-                                              (uint32_t)(base + t * 28 * N * 8), 0, kNtC3 ? 2 : 0);
+                                              (uint32_t)(base + t * 28 * N * 8), 0, kNtW5 ? 2 : 0);
       });
     }
   }
