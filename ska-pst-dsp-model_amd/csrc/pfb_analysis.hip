@@ -432,7 +432,7 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges,
       make_rsrc(xpol + b0, (uint32_t)min(max(avail, (int64_t)0) * 8, kRsrcMaxBytes));
   auto ld = [&](int64_t rho, int col) {  // x[rho N + col]
     const int64_t g = rho * N + col;
-    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (uint32_t)((g - b0) * 8), 0, 0);
+    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(xr, (uint32_t)((g - b0) * 8), 0, kNtlFir ? 2 : 0);
     return __builtin_bit_cast(v2f, v);
   };
   // taps by (new-sample slot i, lag j): padded i + j DE, Bunton PW - DE + i - j DE

@@ -73,6 +73,24 @@ constexpr int kAuxLcbf = PFB_AUX_LCBF;
 #define PFB_NT_W5 1
 #endif
 constexpr bool kNtFirZ = PFB_NT_FIRZ != 0, kNtRow = PFB_NT_ROW != 0, kNtW5 = PFB_NT_W5 != 0;
+// and their loads: the FIR's input (PFB_NTL_FIR), the row FFT's rows (PFB_NTL_ROW), the
+// synth_wave512 stage-1 rows (PFB_NTL_W5): none faster than the default policy
+// (profiles/r04_v9_c3_load_policy_ab.jsonl)
+#ifndef PFB_NTL_FIR
+#define PFB_NTL_FIR 0
+#endif
+#ifndef PFB_NTL_ROW
+#define PFB_NTL_ROW 0
+#endif
+#ifndef PFB_NTL_W5
+#define PFB_NTL_W5 0
+#endif
+constexpr bool kNtlFir = PFB_NTL_FIR != 0, kNtlRow = PFB_NTL_ROW != 0, kNtlW5 = PFB_NTL_W5 != 0;
+template <bool NT>
+__device__ __forceinline__ float2 ld_nt(const float2* p) {
+  if constexpr (NT) return __builtin_bit_cast(float2, __builtin_nontemporal_load(reinterpret_cast<const v2f*>(p)));
+  else return *p;
+}
 template <bool NT>
 __device__ __forceinline__ void st_nt(float2* p, float2 v) {
   if constexpr (NT) __builtin_nontemporal_store(__builtin_bit_cast(v2f, v), reinterpret_cast<v2f*>(p));
@@ -320,7 +338,7 @@ __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
   float2 pf[PF][R];
   auto load_row = [&](int64_t row, float2* d) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) d[r] = in[row * N + col[r]];
+    for (int r = 0; r < R; ++r) d[r] = ld_nt<kNtlRow>(in + row * N + col[r]);
   };
 #pragma unroll
   for (int k = 0; k < PF; ++k) load_row(min(q0 + k, q1 - 1), pf[k]);

@@ -179,7 +179,7 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     static_for<0, R0>([&](auto r) { x[r] = x[r + DK]; });
     const __amdgpu_buffer_rsrc_t z = make_rsrc(zpol + (int64_t)b * a.keep * N, zbytes);
     static_for<R0, 16>([&](auto r) {
-      const v2u v = __builtin_amdgcn_raw_buffer_load_b64(z, zlane, r * 32 * N * 8, 0);
+      const v2u v = __builtin_amdgcn_raw_buffer_load_b64(z, zlane, r * 32 * N * 8, kNtlW5 ? 2 : 0);
       x[r] = __builtin_bit_cast(float2, v);
     });
   };
