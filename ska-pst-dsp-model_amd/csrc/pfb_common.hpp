@@ -298,8 +298,8 @@ __global__ __launch_bounds__(NT) void row_fft_kernel(RowFftArgs a) {
 }
 
 // All passes of FFTPlan<N> after the first (one row, LDS -> ... -> `last`).
-template <int N, int DIR, class Last, int R0, int... Rest>
-__device__ __forceinline__ void run_rest(const LdsRows& lds, const Last& last, const float2* tw, int tid,
+template <int N, int DIR, class Last, class TW, int R0, int... Rest>
+__device__ __forceinline__ void run_rest(const LdsRows& lds, const Last& last, const TW& tw, int tid,
                                          Radices<R0, Rest...>) {
   static_assert(sizeof...(Rest) > 0, "transform has a single pass");
   run_passes_impl<N, DIR, 1, NT, R0, Rest...>(lds, last, lds, tw, tid);
@@ -311,8 +311,13 @@ __device__ __forceinline__ void run_rest(const LdsRows& lds, const Last& last, c
 // columns in registers, and loads row r + 1 into registers while it transforms row r.
 // (The one-shot kernel re-read the 32 KB table from L2 for every one of the 73 400 C3
 // rows and waited for each row's loads with nothing in flight.)
-// PF: rows prefetched ahead (1, or 2 with 32 more VGPRs: 64 KB in flight per workgroup)
-template <int N, int DIR, bool PERM, bool GAIN, int PF = 1>
+// PF: rows prefetched ahead (1, or 2 with 32 more VGPRs: 64 KB in flight per workgroup).
+// HT: half twiddle table (HalfTw: N / 2 entries, 17 KB less LDS per workgroup).
+template <int N>
+constexpr size_t row_fft_persist_lds(bool ht) {
+  return ((size_t)RowShape<N>::RS + tw_slots(ht ? N / 2 : N)) * sizeof(float2);
+}
+template <int N, int DIR, bool PERM, bool GAIN, int PF = 1, bool HT = false>
 __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
   static_assert(RowShape<N>::ROWS == 1, "one row per workgroup");
   constexpr int R = FirstPassOf<N, 1, NT>::R, NB = N / R;
@@ -325,7 +330,7 @@ __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
   const int tid = threadIdx.x;
   LdsRows rows(smem, RowShape<N>::RS);
   float2* tw = smem + RowShape<N>::RS;
-  for (int m = tid; m < N; m += NT) tw[tw_slot(m)] = a.tw[m];
+  for (int m = tid; m < (HT ? N / 2 : N); m += NT) tw[tw_slot(m)] = a.tw[m];
   const float2* in = a.in + pol * a.in_pol_stride;
   int col[R];
   float g[R];
@@ -360,7 +365,8 @@ __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
     __syncthreads();
     RowStore st{a.out + pol * a.out_pol_stride, row, a.n_rows, N, a.sds, a.remap, a.scale,
                 a.row_base, a.n_total};
-    run_rest<N, DIR>(rows, st, tw, tid, typename FFTPlan<N>::type{});
+    if constexpr (HT) run_rest<N, DIR>(rows, st, HalfTw{tw, ilog2(N / 2)}, tid, typename FFTPlan<N>::type{});
+    else run_rest<N, DIR>(rows, st, (const float2*)tw, tid, typename FFTPlan<N>::type{});
   }
 }
 

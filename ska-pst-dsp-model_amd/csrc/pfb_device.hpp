@@ -119,6 +119,7 @@ constexpr int first_factor(int R) {
 }
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+constexpr int ilog2(int n) { return n <= 1 ? 0 : 1 + ilog2(n / 2); }
 // x^{-1} mod m (gcd(x, m) = 1)
 constexpr int cinv_mod(int x, int m) {
   for (int i = 1; i < m; ++i)
@@ -312,8 +313,23 @@ __host__ __device__ constexpr int high_bit(int r) {
   while (2 * h <= r) h *= 2;
   return h;
 }
-template <int R, int DIR>
-__device__ __forceinline__ void twiddle_powers(const float2* __restrict__ tw, int m, float2 (&w)[R]) {
+// Half table (the persistent 4096-point row FFT): entries m < H = N / 2 only, the upper
+// half from e^{-2 pi i (m + H) / N} = -e^{-2 pi i m / N} (a sign flip, exact) — half the LDS,
+// so one more workgroup fits per CU
+struct HalfTw {
+  const float2* p;
+  int h_log2;  // H = 2^h_log2
+};
+template <int DIR>
+__device__ __forceinline__ float2 table_tw(const HalfTw& t, int m) {
+  float2 w = t.p[tw_slot(m & ((1 << t.h_log2) - 1))];
+  const uint32_t sg = ((uint32_t)m >> t.h_log2) << 31;  // m < N: bit h_log2 is the half
+  w.x = __uint_as_float(__float_as_uint(w.x) ^ sg);
+  w.y = __uint_as_float(__float_as_uint(w.y) ^ (DIR > 0 ? sg ^ 0x80000000u : sg));
+  return w;
+}
+template <int R, int DIR, class TW>
+__device__ __forceinline__ void twiddle_powers(const TW& tw, int m, float2 (&w)[R]) {
   static_for<1, R>([&](auto rv) {
     constexpr int r = decltype(rv)::value;
     if constexpr (high_bit(r) == r) w[r] = table_tw<DIR>(tw, r * m);
@@ -330,9 +346,8 @@ __device__ __forceinline__ void twiddle_powers(const float2* __restrict__ tw, in
 // stores through `out`.  All NT threads participate; the pass contains one barrier
 // between its loads and its stores, so `in` and `out` may alias (in-place via
 // registers).  The caller places a barrier before the next pass reads `out`.
-template <int N, int R, int NS, int DIR, int ROWS, int NT, class In, class Out>
-__device__ __forceinline__ void stockham_pass(const In& in, const Out& out,
-                                              const float2* __restrict__ tw, int tid) {
+template <int N, int R, int NS, int DIR, int ROWS, int NT, class In, class Out, class TW>
+__device__ __forceinline__ void stockham_pass(const In& in, const Out& out, const TW& tw, int tid) {
   constexpr int NB = N / R;
   constexpr int TOT = ROWS * NB;
   constexpr int PER = (TOT + NT - 1) / NT;
@@ -371,9 +386,9 @@ struct LdsRows : LdsIO {
 
 // Run all passes of FFTPlan<N>; first pass loads via `first`, last pass stores via
 // `last`, intermediate passes go through the LDS rows `lds`.
-template <int N, int DIR, int ROWS, int NT, int NS, int R, int... Rest, class First, class Last>
+template <int N, int DIR, int ROWS, int NT, int NS, int R, int... Rest, class First, class Last, class TW>
 __device__ __forceinline__ void run_passes_impl(const First& first, const Last& last,
-                                                const LdsRows& lds, const float2* tw, int tid) {
+                                                const LdsRows& lds, const TW& tw, int tid) {
   if constexpr (sizeof...(Rest) == 0) {
     stockham_pass<N, R, NS, DIR, ROWS, NT>(first, last, tw, tid);
   } else {

@@ -15,7 +15,9 @@ static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s
     // persistent workgroups (row_fft_persist_kernel) once there are several rows per
     // resident workgroup; PFB_ROWFFT_PERSIST=0: one workgroup per row (A/B)
     static const bool off = knob("PFB_ROWFFT_PERSIST") && std::atoi(knob("PFB_ROWFFT_PERSIST")) == 0;
-    const size_t bytes = ((size_t)RowShape<N>::RS + tw_slots(N)) * sizeof(float2);
+    // (PFB_ROWFFT_HT=1: half twiddle table, experiments A/B)
+    static const bool ht = kExperiments && knob("PFB_ROWFFT_HT") && std::atoi(knob("PFB_ROWFFT_HT")) == 1;
+    const size_t bytes = row_fft_persist_lds<N>(ht);
     const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / bytes);
     int64_t wgs = (int64_t)cu_count() * per_cu;
     // (PFB_ROWFFT_WGS: fewer persistent workgroups, so the row FFT can share the chip with
@@ -28,6 +30,7 @@ static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s
       if constexpr (kExperiments) {
         static const bool pf2 = knob("PFB_ROWFFT_PF") && std::atoi(knob("PFB_ROWFFT_PF")) == 2;
         if (pf2) kern = row_fft_persist_kernel<N, DIR, PERM, GAIN, 2>;
+        if (ht) kern = row_fft_persist_kernel<N, DIR, PERM, GAIN, 1, true>;
       }
       hipError_t e = set_lds(kern, bytes);
       if (e != hipSuccess) return e;
