@@ -51,7 +51,18 @@ bool synth_wave_fir_supported(const SynthBlockArgs& a) {
 
 template <int RW, bool SPANS, bool XW, class FIRV = NoFir, bool WFLAT = false>
 static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
-  auto kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT>;
+  // the XW kernels raise their issue priority from the loop-top barrier to the swap-1
+  // barrier (PRIO 1): a workgroup's waves reach the cross-wave exchange together instead of
+  // trailing the other two resident workgroups' waves (C2 synthesis 63.6-65.6 -> 61.9-62.8
+  // us, profiles/r04_v11_wave_prio_ab.jsonl)
+  auto kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, XW ? 1 : 0>;
+  if constexpr (kExperiments && RW == 14 && SPANS && XW && WFLAT) {
+    // (PFB_WAVE_PRIO=0/2/3: other priority schedules, experiments build only)
+    static const int prio = knob("PFB_WAVE_PRIO") ? std::atoi(knob("PFB_WAVE_PRIO")) : 1;
+    if (prio == 0) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 0>;
+    if (prio == 2) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 2>;
+    if (prio == 3) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 3>;
+  }
   hipError_t e = set_lds(kern, kLdsB);
   if (e != hipSuccess) return e;
   const int groups = a.N / kCols;

@@ -100,7 +100,11 @@ struct RangeSched {
 // WFLAT: the temporal window is exactly 1 on rows [48, 208) of the block (tukey with Ov <= 48,
 // SynthBlockArgs::win_flat): registers r = 3 .. 12 (rows l + 16 r) skip the multiply — the
 // product by 1 is exact, so the output is bit-identical
-template <int RW, bool SPANS, int DK, class SCHED, bool XW = false, class FIRV = NoFir, bool WFLAT = false>
+// PRIO (bit mask): raise the wave's issue priority (s_setprio 2) between the loop-top
+// barrier and the swap-1 barrier (1), and / or from the swap-2 barrier to the block's
+// stores (2)
+template <int RW, bool SPANS, int DK, class SCHED, bool XW = false, class FIRV = NoFir, bool WFLAT = false,
+          int PRIO = 0>
 __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol, int tg, const SCHED& sch) {
   constexpr int W = 16 * RW;
   static_assert(RW <= 14 && RW % 2 == 0, "W = 16 RW with RW even and <= 14");
@@ -267,6 +271,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     // every wave may load them after it)
     if (wave == 0 && i + 1 < nb) sch.wait(sch.block(i + 1));
     __syncthreads();
+    if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(2);
     // ---- pass 1: taper, 16-point DFT over r, twiddle
     float2 v[16];
     if constexpr (WFLAT) {
@@ -305,6 +310,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       constexpr int fr = decltype(f)::value;
       *reinterpret_cast<float2*>(lds + wr1 + fr * kRowB) = v[fr];
     });
+    if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(0);
     if constexpr (XW) __syncthreads();  // the phase tiles were written by every wave
     else __builtin_amdgcn_wave_barrier();
     static_for<0, 8>([&](auto k) {
@@ -331,6 +337,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       *reinterpret_cast<float2*>(lds + wr + tr * kRowB) = u[tr];
     });
     __syncthreads();
+    if constexpr (PRIO & 2) __builtin_amdgcn_s_setprio(2);
     static_for<0, 8>([&](auto k) {
       lds_pair(lds + rd2 + 16 * k, v[2 * k], v[2 * k + 1]);
     });
@@ -352,6 +359,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
                                               (uint32_t)(base + t * RW * N * 8), 0, kAuxOut);
       });
     }
+    if constexpr (PRIO & 2) __builtin_amdgcn_s_setprio(0);
     if constexpr (FIRV::kOn) {
       if (i + 1 < nb) {  // uniform per workgroup
         // the next block: its first RL register rows are this block's last, the others come
@@ -369,7 +377,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
   }
 }
 
-template <int RW, bool SPANS, int DK, bool XW = false, class FIRV = NoFir, bool WFLAT = false>
+template <int RW, bool SPANS, int DK, bool XW = false, class FIRV = NoFir, bool WFLAT = false, int PRIO = 0>
 __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(3)))
 void synth_wave_kernel(SynthBlockArgs a) {
   const int groups = a.N / kCols;
@@ -378,7 +386,7 @@ void synth_wave_kernel(SynthBlockArgs a) {
   const int Rg = gridDim.x / groups;
   const int b_begin = (int)((int64_t)a.n_blocks * rr / Rg);
   const int b_end = (int)((int64_t)a.n_blocks * (rr + 1) / Rg);
-  synth_wave_body<RW, SPANS, DK, RangeSched, XW, FIRV, WFLAT>(a, blockIdx.y, lt % groups,
+  synth_wave_body<RW, SPANS, DK, RangeSched, XW, FIRV, WFLAT, PRIO>(a, blockIdx.y, lt % groups,
                                                               RangeSched{b_begin, b_end - b_begin});
 }
 
