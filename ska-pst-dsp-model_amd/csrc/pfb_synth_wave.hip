@@ -62,6 +62,8 @@ static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
     if (prio == 0) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 0>;
     if (prio == 2) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 2>;
     if (prio == 3) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 3>;
+    if (prio == 4) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 4>;
+    if (prio == 5) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 5>;
   }
   hipError_t e = set_lds(kern, kLdsB);
   if (e != hipSuccess) return e;

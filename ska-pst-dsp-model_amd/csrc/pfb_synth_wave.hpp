@@ -101,8 +101,8 @@ struct RangeSched {
 // SynthBlockArgs::win_flat): registers r = 3 .. 12 (rows l + 16 r) skip the multiply — the
 // product by 1 is exact, so the output is bit-identical
 // PRIO (bit mask): raise the wave's issue priority (s_setprio 2) between the loop-top
-// barrier and the swap-1 barrier (1), and / or from the swap-2 barrier to the block's
-// stores (2)
+// barrier and the swap-1 barrier (1), from the swap-2 barrier to the block's stores (2),
+// from the swap-1 barrier to the swap-2 barrier (4)
 template <int RW, bool SPANS, int DK, class SCHED, bool XW = false, class FIRV = NoFir, bool WFLAT = false,
           int PRIO = 0>
 __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol, int tg, const SCHED& sch) {
@@ -312,6 +312,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     });
     if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(0);
     if constexpr (XW) __syncthreads();  // the phase tiles were written by every wave
+    if constexpr (PRIO & 4) __builtin_amdgcn_s_setprio(2);
     else __builtin_amdgcn_wave_barrier();
     static_for<0, 8>([&](auto k) {
       lds_pair(lds + rd1 + 16 * k, v[2 * k], v[2 * k + 1]);
@@ -336,6 +337,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       constexpr int tr = decltype(t)::value;
       *reinterpret_cast<float2*>(lds + wr + tr * kRowB) = u[tr];
     });
+    if constexpr (PRIO & 4) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
     if constexpr (PRIO & 2) __builtin_amdgcn_s_setprio(2);
     static_for<0, 8>([&](auto k) {

@@ -84,7 +84,9 @@ __device__ __forceinline__ void twiddle_rows(float2* v, const char* row) {
 // rows x 2 phases, and swap 1 crosses waves (one more workgroup barrier per block)
 // WFLAT: the temporal window is exactly 1 on rows [128, 384) (tukey with Ov <= 128,
 // SynthBlockArgs::win_flat): registers r = 4 .. 11 (rows m + 32 r) skip the multiply (exact)
-template <bool SPANS, bool XW, bool WFLAT = false>
+// PRIO: as synth_wave_kernel (1: issue priority 2 from the loop-top barrier to the swap-1
+// barrier)
+template <bool SPANS, bool XW, bool WFLAT = false, int PRIO = 0>
 __global__ __launch_bounds__(kW5Threads) __attribute__((amdgpu_waves_per_eu(3)))
 void synth_wave512_kernel(SynthBlockArgs a) {
   constexpr int W = 448, DK = 8;  // keep = 256 rows = 8 register rows of 32
@@ -190,6 +192,7 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     const int b = b_begin + i;
     // every wave has read the previous block's swap-2 data (from all tiles)
     __syncthreads();
+    if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(2);
     // ---- pass 1: taper, 16-point DFT over r, x w_512^{m f1}
     float2 v[16];
     if constexpr (WFLAT) {
@@ -220,6 +223,7 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     static_for<0, 16>([&](auto f) {
       *reinterpret_cast<float2*>(lds + wr1 + decltype(f)::value * (2 * kRowB)) = v[decltype(f)::value];
     });
+    if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(0);
     if constexpr (XW) __syncthreads();  // the phase tiles were written by every wave
     else __builtin_amdgcn_wave_barrier();
     static_for<0, 8>([&](auto k) { lds_pair2(lds + rd1 + 16 * k, v[2 * k], v[2 * k + 1]); });
@@ -280,6 +284,11 @@ bool synth_wave512_supported(const SynthBlockArgs& a) {
 template <bool SPANS, bool XW, bool WFLAT = false>
 static hipError_t launch_w5(const SynthBlockArgs& a, hipStream_t s) {
   auto kern = synth_wave512_kernel<SPANS, XW, WFLAT>;
+  if constexpr (kExperiments && XW && WFLAT) {
+    // (PFB_W5_PRIO=1: issue-priority A/B, experiments build only)
+    static const int prio = knob("PFB_W5_PRIO") ? std::atoi(knob("PFB_W5_PRIO")) : 0;
+    if (prio == 1) kern = synth_wave512_kernel<SPANS, XW, WFLAT, 1>;
+  }
   hipError_t e = set_lds(kern, kW5LdsB);
   if (e != hipSuccess) return e;
   const int groups = a.N / kW5Cols;
