@@ -64,6 +64,8 @@ static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
     if (prio == 3) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 3>;
     if (prio == 4) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 4>;
     if (prio == 5) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 5>;
+    if (prio == 8) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 8>;
+    if (prio == 16) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 16>;
   }
   hipError_t e = set_lds(kern, kLdsB);
   if (e != hipSuccess) return e;

@@ -102,7 +102,7 @@ struct RangeSched {
 // product by 1 is exact, so the output is bit-identical
 // PRIO (bit mask): raise the wave's issue priority (s_setprio 2) between the loop-top
 // barrier and the swap-1 barrier (1), from the swap-2 barrier to the block's stores (2),
-// from the swap-1 barrier to the swap-2 barrier (4)
+// from the swap-1 barrier to the swap-2 barrier (4); 8 / 16: as 1 with priority 3 / 1
 template <int RW, bool SPANS, int DK, class SCHED, bool XW = false, class FIRV = NoFir, bool WFLAT = false,
           int PRIO = 0>
 __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol, int tg, const SCHED& sch) {
@@ -272,6 +272,8 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     if (wave == 0 && i + 1 < nb) sch.wait(sch.block(i + 1));
     __syncthreads();
     if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(2);
+    if constexpr (PRIO & 8) __builtin_amdgcn_s_setprio(3);
+    if constexpr (PRIO & 16) __builtin_amdgcn_s_setprio(1);
     // ---- pass 1: taper, 16-point DFT over r, twiddle
     float2 v[16];
     if constexpr (WFLAT) {
@@ -310,7 +312,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       constexpr int fr = decltype(f)::value;
       *reinterpret_cast<float2*>(lds + wr1 + fr * kRowB) = v[fr];
     });
-    if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO & 25) __builtin_amdgcn_s_setprio(0);
     if constexpr (XW) __syncthreads();  // the phase tiles were written by every wave
     if constexpr (PRIO & 4) __builtin_amdgcn_s_setprio(2);
     else __builtin_amdgcn_wave_barrier();
