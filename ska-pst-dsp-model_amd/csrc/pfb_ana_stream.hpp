@@ -63,9 +63,7 @@ struct ColMajorLds {
 // column (AnalysisArgs::zblk) for the synthesis wave kernel.
 // Streaming analysis of step range w of nw (steps of T rows from row0) for polarisation
 // pol.
-// PRIO (experiments A/B): 1 = issue priority 2 while the step's prefetch loads issue,
-// 2 = from the FFT barrier to the end of the step
-template <int N, int P, int NU, int DE, int ZOUT, bool LCBF, bool GS, int PRIO = 0>
+template <int N, int P, int NU, int DE, int ZOUT, bool LCBF, bool GS>
 __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int pol, int w, int nw) {
   using SH = StreamShape<N, P, NU, DE>;
   constexpr int M = SH::M, PE = SH::PE, QS = SH::QS, T = SH::T, NEW = SH::NEW, WIN = SH::WIN;
@@ -135,10 +133,8 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
     // a conditional prefetch makes vmcnt path-dependent and the next step waits for
     // every store as well)
     v2f pf[NEW];
-    if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
     for (int i = 0; i < NEW; ++i) pf[i] = ld(rel + WIN + i);
-    if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(0);
     __syncthreads();  // previous step's FFT has read its rows (first step: F staged)
     // all NU x QS rows accumulate together (tap-outer order): consecutive FMAs are
     // independent, so the 4-cycle FMA latency never stalls issue
@@ -196,7 +192,6 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
       });
     });
     __syncthreads();
-    if constexpr (PRIO & 2) __builtin_amdgcn_s_setprio(2);
     if constexpr (LCBF) {
       const LcbfRowStore st = LcbfRowStore::rows(opol, k0, T, a.row0, a.K, a.lcbf_scale);
       block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
@@ -237,7 +232,6 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
       const BufRowStore st = BufRowStore::rows(opol, k0, T, a.row0, a.K, N, (float)N);
       block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
     }
-    if constexpr (PRIO & 2) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
     for (int i = 0; i < PE - 1; ++i) win[i] = win[i + NEW];
 #pragma unroll
@@ -245,10 +239,9 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
   }
 }
 
-template <int N, int P, int NU, int DE, int ZOUT, bool LCBF = false, bool GS = false, int PRIO = 0>
+template <int N, int P, int NU, int DE, int ZOUT, bool LCBF = false, bool GS = false>
 __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
-  analysis_stream_body<N, P, NU, DE, ZOUT, LCBF, GS, PRIO>(a, blockIdx.y, xcd_tile(blockIdx.x, gridDim.x),
-                                                           gridDim.x);
+  analysis_stream_body<N, P, NU, DE, ZOUT, LCBF, GS>(a, blockIdx.y, xcd_tile(blockIdx.x, gridDim.x), gridDim.x);
 }
 
 }  // namespace pfb

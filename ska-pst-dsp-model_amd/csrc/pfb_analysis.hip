@@ -663,15 +663,6 @@ static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
                                      : analysis_stream_kernel<N, P, NU, DE, 1>)
               : a.out_rs > 0 ? analysis_stream_kernel<N, P, NU, DE, 0, false, true>
                              : analysis_stream_kernel<N, P, NU, DE, 0>;
-  if constexpr (kExperiments) {
-    // (PFB_ANA_PRIO=1/2/3: issue-priority A/B of the round trip's analysis, experiments only)
-    static const int prio = knob("PFB_ANA_PRIO") ? std::atoi(knob("PFB_ANA_PRIO")) : 0;
-    if (!LCBF && a.z && a.zblk == 2) {
-      if (prio == 1) kern = analysis_stream_kernel<N, P, NU, DE, 2, false, false, 1>;
-      if (prio == 2) kern = analysis_stream_kernel<N, P, NU, DE, 2, false, false, 2>;
-      if (prio == 3) kern = analysis_stream_kernel<N, P, NU, DE, 2, false, false, 3>;
-    }
-  }
   // the carry (pre) is read only in each workgroup's first WIN-row window prologue: every
   // pad sample must lie inside the first window (the caller's B <= P N guard)
   if (a.pre && (a.pad < 0 || a.pad > (int64_t)SH::WIN * N)) return hipErrorInvalidValue;
