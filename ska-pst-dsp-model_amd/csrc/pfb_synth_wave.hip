@@ -66,6 +66,8 @@ static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
     if (prio == 5) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 5>;
     if (prio == 8) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 8>;
     if (prio == 16) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 16>;
+    if (prio == 32) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 32>;
+    if (prio == 33) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 33>;
   }
   hipError_t e = set_lds(kern, kLdsB);
   if (e != hipSuccess) return e;

@@ -102,7 +102,8 @@ struct RangeSched {
 // product by 1 is exact, so the output is bit-identical
 // PRIO (bit mask): raise the wave's issue priority (s_setprio 2) between the loop-top
 // barrier and the swap-1 barrier (1), from the swap-2 barrier to the block's stores (2),
-// from the swap-1 barrier to the swap-2 barrier (4); 8 / 16: as 1 with priority 3 / 1
+// from the swap-1 barrier to the swap-2 barrier (4); 8 / 16: as 1 with priority 3 / 1;
+// 32: the loop-top barrier moved below pass 1
 template <int RW, bool SPANS, int DK, class SCHED, bool XW = false, class FIRV = NoFir, bool WFLAT = false,
           int PRIO = 0>
 __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol, int tg, const SCHED& sch) {
@@ -270,7 +271,9 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     // (fused round trip: one wave waits for the next block's rows before the barrier, so
     // every wave may load them after it)
     if (wave == 0 && i + 1 < nb) sch.wait(sch.block(i + 1));
-    __syncthreads();
+    // (PRIO & 32: this barrier moves down to just before the swap-1 writes — pass 1 touches
+    // only the constant tables in LDS, so it may overlap other waves' pass 3)
+    if constexpr (!(PRIO & 32)) __syncthreads();
     if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(2);
     if constexpr (PRIO & 8) __builtin_amdgcn_s_setprio(3);
     if constexpr (PRIO & 16) __builtin_amdgcn_s_setprio(1);
@@ -307,6 +310,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       static_for<0, 8>([&](auto k) { lds_pair(tw1row + 16 * k, w[2 * k], w[2 * k + 1]); });
       static_for<1, 16>([&](auto f) { v[f] = cmul(v[f], w[f]); });
     }
+    if constexpr ((PRIO & 32) != 0) __syncthreads();
     // ---- swap 1 (inside the wave): element (row f1, slot l) of this phase's tile
     static_for<0, 16>([&](auto f) {
       constexpr int fr = decltype(f)::value;
