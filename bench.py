@@ -96,6 +96,14 @@ def parse():
                     help="synthesis stage-1 rows of the fused round trip "
                          "(pfb_synthesis_set_stage1_rows): written by the analysis and read back, "
                          "or recomputed from the input by the synthesis (bit-identical output)")
+    ap.add_argument("--c3", type=int, default=1,
+                    help="N=1 only: also time BASELINE configs[2] (C3 SKA-Mid padded round trip, "
+                         "4096 ch, 100 353 taps, 2^26 samples) as the line's `c3` key (not the "
+                         "headline value)")
+    ap.add_argument("--synthesis-only", type=int, default=1,
+                    help="N=1 only: also time the standalone synthesis of an HBM-resident C2 "
+                         "channelised product (SynthesisPlan.execute: channel IFFT + synthesis, "
+                         "the PST InverseFilterBank case) as the line's `synthesis_only` key")
     ap.add_argument("--e2e", type=int, default=0,
                     help="also time the host-buffer path: pinned DADA bytes (NBIT 8 TFP) -> "
                          "H2D -> unpack -> round trip -> pack (NBIT 32) -> D2H (reported as "
@@ -200,6 +208,34 @@ def cpu_baseline(budget_s: float, workers: int):
     else:
         out.update(value=one["value"], cores=1, sample=one["sample"] + " (NumPy oracle, 1 core)")
     return out
+
+
+C3_N_CHAN, C3_TAPS_PER_CHAN, C3_NF, C3_OV = 4096, 28, 512, 128
+C3_N_DAT = 1 << 26
+C3_CPU_UNIT = 1 << 22  # bounded CPU sample of C3: 2^22 samples = 2 synthesis blocks
+
+
+def c3_taps():
+    from ska_pst_dsp_model_amd import firio
+    return firio.design_PFB_FIR_filter_two_stage(C3_N_CHAN, OS_STR, C3_TAPS_PER_CHAN)
+
+
+def cpu_baseline_c3(taps):
+    """The oracle's C3 round trip (polyphase_analysis_padded -> polyphase_synthesis,
+    complex64, numpy.fft, one core) on a bounded 2^22-sample sample of the C3 unit."""
+    from oracle import pfb_oracle as orc
+    rng = np.random.default_rng(3)
+    x = ((rng.standard_normal((1, 1, C3_CPU_UNIT)) + 1j * rng.standard_normal((1, 1, C3_CPU_UNIT))) /
+         np.sqrt(2)).astype(np.complex64)
+    win = orc.pfb_window("tukey", C3_NF, C3_OV)
+    dr = {"apply_deripple": 1, "filter_coeff": taps}
+    t0 = time.perf_counter()
+    chan = orc.polyphase_analysis_padded(x, taps, C3_N_CHAN, OS_STR, dtype=np.complex64)
+    orc.polyphase_synthesis(chan, 1, C3_NF, OS_STR, dr, 1, C3_OV, win, dtype=np.complex64)
+    el = time.perf_counter() - t0
+    return {"value": round(C3_CPU_UNIT / el / 1e6, 3), "unit": "complex Msamples/s", "cores": 1,
+            "kind": "port", "sample": f"one 2^22-sample C3 unit (2 synthesis blocks), NumPy oracle "
+                                      f"round trip, complex64, {el:.1f} s"}
 
 
 def copy_rate(torch, dev, lib, n_bytes: int = 1 << 31, reps: int = 20):
@@ -383,6 +419,12 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_workers or cpu_workers_default())
+    # C3 (N = 1 only): its taps (plan-time firls design, a few seconds) and its CPU leg
+    c3 = None
+    if world == 1 and args.c3 and not args.stub_device:
+        c3 = {"taps": c3_taps()}
+        if not args.no_cpu_baseline:
+            c3["cpu_baseline"] = cpu_baseline_c3(c3["taps"])
 
     import torch
     import torch.distributed as dist
@@ -395,7 +437,7 @@ def main():
         if world > 1:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        res = run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds)
+        res = run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds, c3)
 
     all_seeds = gather_seeds(dist, world, pair_seeds(seeds, args.inflight, args.distinct_inputs),
                              args.stub_device, torch, local)
@@ -454,7 +496,116 @@ def run_stub(args, world, dist):
             "taps": 3073, "K": 0, "n_out": 0}
 
 
-def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
+PROFILE_CLASSES = ["analysis", "synth_chan_ifft", "synth_block", "analysis+chan_ifft", "fir", "row_fft"]
+
+
+def read_profile(lib, steps):
+    """Per-kernel-class HIP-event timings recorded since pfb_profile_reset (on the
+    library's launch stream): {class: {kernel, avg_ms, launches, alg_bytes_per_launch,
+    ms_per_step}}."""
+    import ctypes
+    kern = {}
+    for w, name in enumerate(PROFILE_CLASSES):
+        ms, nl, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        lib.pfb_profile_read(w, ctypes.byref(ms), ctypes.byref(nl), ctypes.byref(by))
+        if nl.value:
+            buf = ctypes.create_string_buffer(512)
+            lib.pfb_profile_kernel_name(w, buf, len(buf))
+            kern[name] = {"kernel": buf.value.decode() or None,
+                          "avg_ms": ms.value / nl.value, "launches": nl.value,
+                          "alg_bytes_per_launch": by.value / nl.value,
+                          "ms_per_step": ms.value / steps}
+    return kern
+
+
+def measure_c3(args, torch, dist, world, dev, pfb, lib, c3):
+    """BASELINE configs[2]: SKA-Mid padded round trip — 4096 channels, OS
+    8/7, 100 353 two-stage firls taps, 2^26 samples, Nf 512, Ov 128, tukey, deripple —
+    through pfb_roundtrip_execute (FIR -> row FFT -> synthesis), input resident in HBM.
+    K timed steps between barrier + synchronize, then the same K with HIP events around
+    every kernel (per-kernel durations and the roofline)."""
+    taps = c3["taps"]
+    g = torch.Generator(device=dev).manual_seed(300)
+    x = (torch.complex(torch.randn((1, C3_N_DAT), device=dev, generator=g),
+                       torch.randn((1, C3_N_DAT), device=dev, generator=g)) / np.sqrt(2.0)).to(torch.complex64)
+    win = pfb.PFBWindow().lookup["tukey"](C3_NF, C3_OV)
+    ana = pfb.AnalysisPlan(taps, C3_N_CHAN, OS_STR, "polyphase_analysis_padded", 1, dev.index or 0)
+    syn = pfb.SynthesisPlan(C3_N_CHAN, OS_STR, C3_NF, C3_OV, True, 1, True, taps, win, None, 1, dev.index or 0)
+    K = ana.output_length(C3_N_DAT)
+    n_out = syn.output_length(K)
+    chan = torch.empty((1, K, C3_N_CHAN), dtype=torch.complex64, device=dev)
+    out = torch.empty((1, n_out), dtype=torch.complex64, device=dev)
+
+    def step():
+        pfb.roundtrip(ana, syn, x, chan=chan, out=out)
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize(dev)
+    el = timed_region(args.steps, step, world, dist, lambda: torch.cuda.synchronize(dev))
+    lib.pfb_profile_reset()
+    lib.pfb_profile_enable(1)
+    timed_region(args.steps, step, world, dist, lambda: torch.cuda.synchronize(dev))
+    lib.pfb_profile_enable(0)
+    kern = read_profile(lib, args.steps)
+    lib.pfb_profile_reset()
+    ms = el / args.steps * 1e3
+    b_alg = 16.0 * (1.0 + 8.0 / 7.0) * C3_N_DAT  # x in + chan out + chan in + output out
+    gbs = b_alg / (ms * 1e-3) / 1e9
+    res = {"workload": "C3 SKA-Mid padded round trip: 4096 ch, OS 8/7, %d two-stage firls taps, 2^26 "
+                       "samples, Nf 512, Ov 128, tukey, deripple; 1 single-pol unit" % len(taps),
+           "ms": round(ms, 4), "value": round(C3_N_DAT / (ms * 1e-3) / 1e6, 2),
+           "unit": "complex Msamples/s", "steps": args.steps, "channelised_rows": K,
+           "output_samples": n_out,
+           "roofline": {"bound": "hbm", "alg_bytes_per_step": b_alg, "achieved": round(gbs, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)},
+           "kernels": kern}
+    del x, chan, out
+    ana.close()
+    syn.close()
+    torch.cuda.empty_cache()
+    return res
+
+
+def measure_synthesis_only(args, torch, dist, world, dev, pfb, lib, ana, taps, x):
+    """The standalone synthesis of a C2 channelised product resident in HBM —
+    SynthesisPlan.execute(chan) = pfb_synthesis_execute: the channel IFFT (stage-1 rows)
+    then the synthesis kernel; the PST production case, CBF-channelised input ->
+    InverseFilterBank (InverseFilterBank.m:92-96, polyphase_synthesis.m:163-316)."""
+    chan = ana.execute(x).contiguous()  # (n_pol, K, N) time-major, written by the analysis
+    win = pfb.PFBWindow().lookup["tukey"](NF, OV)
+    syn = pfb.SynthesisPlan(N_CHAN, OS_STR, NF, OV, True, 1, True, taps, win, None, chan.shape[0], dev.index or 0)
+    K = chan.shape[1]
+    n_out = syn.output_length(K)
+
+    def step():
+        syn.execute(chan, layout="ptc")
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize(dev)
+    el = timed_region(args.steps, step, world, dist, lambda: torch.cuda.synchronize(dev))
+    lib.pfb_profile_reset()
+    lib.pfb_profile_enable(1)
+    timed_region(args.steps, step, world, dist, lambda: torch.cuda.synchronize(dev))
+    lib.pfb_profile_enable(0)
+    kern = read_profile(lib, args.steps)
+    lib.pfb_profile_reset()
+    ms = el / args.steps * 1e3
+    n_pol = chan.shape[0]
+    b_alg = 8.0 * n_pol * (K * N_CHAN + n_out)  # channelised product in + output out
+    gbs = b_alg / (ms * 1e-3) / 1e9
+    res = {"workload": "C2 synthesis only: (n_pol, %d, 256) channelised product of the C2 unit -> "
+                       "%d output samples per pol (Nf 256, Ov 48, tukey, deripple)" % (K, n_out),
+           "ms": round(ms, 4), "value": round(n_pol * n_out / (ms * 1e-3) / 1e6, 2),
+           "unit": "complex Msamples/s (output samples)", "steps": args.steps,
+           "roofline": {"bound": "hbm", "alg_bytes_per_step": b_alg, "achieved": round(gbs, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)},
+           "kernels": kern}
+    del chan
+    syn.close()
+    return res
+
+
+def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds, c3=None):
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -596,19 +747,7 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
     lib.pfb_profile_enable(0)
 
     # per-kernel-class event timings (on the library's launch stream)
-    import ctypes
-    names = ["analysis", "synth_chan_ifft", "synth_block", "analysis+chan_ifft"]
-    kern = {}
-    for w in range(4):
-        ms, nl, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
-        lib.pfb_profile_read(w, ctypes.byref(ms), ctypes.byref(nl), ctypes.byref(by))
-        if nl.value:
-            buf = ctypes.create_string_buffer(512)
-            lib.pfb_profile_kernel_name(w, buf, len(buf))
-            kern[names[w]] = {"kernel": buf.value.decode() or None,
-                              "avg_ms": ms.value / nl.value, "launches": nl.value,
-                              "alg_bytes_per_launch": by.value / nl.value,
-                              "ms_per_step": ms.value / args.steps}
+    kern = read_profile(lib, args.steps)
 
     # A second reading of each kernel's duration: the step's halves (split round trip, pair 0)
     # launched K times back to back on torch's current stream — the library's launch stream —
@@ -644,8 +783,19 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds):
     if args.e2e:
         e2e = e2e_pcie(torch, dev, pfb, ana, syn, n_pol, n_dat, chan_buf, out_buf, args.steps,
                        world, dist)
+    # secondary keys of the N = 1 line (after the headline's regions; never its value)
+    syn_only = c3_res = None
+    if world == 1 and args.synthesis_only:
+        syn_only = measure_synthesis_only(args, torch, dist, world, dev, pfb, lib, ana, taps, x)
+    if world == 1 and c3 is not None:
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        c3_res = measure_c3(args, torch, dist, world, dev, pfb, lib, c3)
+        if "cpu_baseline" in c3:
+            c3_res["cpu_baseline"] = c3["cpu_baseline"]
     return {"el": el, "el_prof": el_prof, "el_serial": el_serial, "kern": kern, "copy_gbs": copy_gbs,
-            "e2e": e2e, "taps": len(taps), "K": K, "n_out": n_out}
+            "e2e": e2e, "taps": len(taps), "K": K, "n_out": n_out, "synthesis_only": syn_only,
+            "c3": c3_res}
 
 
 def report(args, res, world, workload, n_pol, n_dat, all_seeds):
@@ -710,6 +860,18 @@ def report(args, res, world, workload, n_pol, n_dat, all_seeds):
         "ms_per_step_with_kernel_events": round(res["el_prof"] / args.steps * 1e3, 4),
         "kernels": kern,
     }
+    traffic_all = pmc_traffic()
+    for kc in kern.values():  # PMC HBM bytes per launch of every timed kernel class
+        kc["traffic"], _ = traffic_for(workload, kc.get("kernel"), traffic_all)
+    for key, wl in (("synthesis_only", "synthesis_only"), ("c3", "c3")):
+        sec = res.get(key)
+        if sec is None:
+            continue
+        for kc in sec.get("kernels", {}).values():
+            kc["traffic"], _ = traffic_for(wl, kc.get("kernel"), traffic_all)
+            if kc["avg_ms"] > 0:
+                kc["achieved_GBs"] = round(kc["alg_bytes_per_launch"] / (kc["avg_ms"] * 1e-3) / 1e9, 1)
+        out[key] = sec
     out["pfb_env"] = pfb_env()
     if args.stub_device:
         out["stub_device"] = True

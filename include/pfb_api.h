@@ -191,6 +191,12 @@ pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* plan, const pfb_cf
                                           int64_t* n_out, int32_t mem, void* stream);
 int64_t pfb_inverse_filterbank_buffered(const pfb_synthesis_plan* plan);
 pfb_status pfb_inverse_filterbank_reset(pfb_synthesis_plan* plan);
+/* InverseFilterBank.sample_offset (InverseFilterBank.m:12, 0-based, default 0): every
+ * pfb_inverse_filterbank_execute call synthesises the concatenated rows (carry + input)
+ * from row sample_offset on — polyphase_synthesis(..., sample_offset+1, ...) at :92-96 —
+ * while the carry still starts at the consumed blocks' end (:104-133), so the offset is
+ * skipped again at the head of every call's concatenation, as the Matlab object does. */
+pfb_status pfb_inverse_filterbank_set_sample_offset(pfb_synthesis_plan* plan, int64_t sample_offset);
 
 /* Blocks processed per channel-IFFT/block-kernel chunk (scratch = chunk * keep rows). */
 pfb_status pfb_synthesis_set_chunk_blocks(pfb_synthesis_plan* plan, int32_t blocks);
@@ -210,6 +216,11 @@ typedef enum pfb_stage1_rows {
   PFB_STAGE1_RECOMPUTED = 2
 } pfb_stage1_rows;
 pfb_status pfb_synthesis_set_stage1_rows(pfb_synthesis_plan* plan, int32_t mode);
+/* Where the plan's last synthesis launch got its stage-1 rows: PFB_STAGE1_STORED (read
+ * from rows a channel IFFT or the analysis wrote), PFB_STAGE1_RECOMPUTED (evaluated from
+ * the input series), 0 before any launch, -1 for a null plan.  A diagnostic: a caller that
+ * asked for RECOMPUTED can tell whether the shape took it (no reference counterpart). */
+int32_t pfb_synthesis_last_stage1_rows(const pfb_synthesis_plan* plan);
 
 /* ---------------------------------------------------------------- round trip */
 /* Analysis followed by synthesis of its output — replaces the analysis -> synthesis
@@ -333,7 +344,9 @@ pfb_status pfb_device_copy(void* dst, const void* src, int64_t n_bytes, void* st
 /* Kernel timing: average duration (ms) of the named kernel class over the launches
  * recorded since the last reset, measured with HIP events on the plan's stream.
  * which: 0 = analysis, 1 = synthesis channel-IFFT, 2 = synthesis block kernel,
- *        3 = analysis fused with the synthesis channel IFFT (pfb_roundtrip_execute). */
+ *        3 = analysis fused with the synthesis channel IFFT (pfb_roundtrip_execute),
+ *        4 / 5 = the FIR / the row FFT of the n_chan > 256 round trip (SKA-Mid), each
+ *        launch timed alone; bytes: what each reads + writes once. */
 pfb_status pfb_profile_enable(int32_t enable);
 pfb_status pfb_profile_read(int32_t which, double* total_ms, int64_t* launches, double* bytes);
 pfb_status pfb_profile_reset(void);

@@ -92,10 +92,13 @@ struct Profiler {
   bool enabled = false;
   std::vector<ProfRec> pending;
   std::vector<hipEvent_t> pool;
-  double total_ms[4] = {0, 0, 0, 0};  // 0 analysis, 1 chan IFFT, 2 block, 3 analysis + chan IFFT
-  int64_t launches[4] = {0, 0, 0, 0};
-  double bytes[4] = {0, 0, 0, 0};
-  std::string names[4];  // kernel of each class's last single-kernel launch (demangled)
+  // 0 analysis, 1 chan IFFT, 2 block, 3 analysis + chan IFFT, 4 / 5 the FIR / row FFT of
+  // the generic (N > 256) round trip (launched one by one so each is timed alone)
+  static constexpr int kClasses = 6;
+  double total_ms[kClasses] = {};
+  int64_t launches[kClasses] = {};
+  double bytes[kClasses] = {};
+  std::string names[kClasses];  // kernel of each class's last single-kernel launch (demangled)
   hipEvent_t get() {
     if (!pool.empty()) {
       hipEvent_t e = pool.back();
@@ -288,8 +291,14 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   // (with z: the stage-1 rows are a synthesis intermediate, not algorithmic bytes —
   // the synthesis' algorithmic read of its input is counted by the block kernel)
   const double bytes = (double)p->n_pol * (8.0 * in_samples + 8.0 * (K_end - row0) * p->N);
-  // generic path = FIR + row FFT launches (z_stage 1 / 2: one of them)
-  ProfScope ps(z ? 3 : 0, bytes, s, p->fused || z_stage != 0);
+  // generic path = FIR + row FFT launches (z_stage 1 / 2: one of them, timed as its own
+  // class; their bytes: the FIR reads the input and writes the stage-1 rows, the row FFT
+  // reads them and writes the channelised product)
+  const double zrow_bytes = (double)p->n_pol * 8.0 * (K_end - row0) * p->N;
+  const int cls = !z ? 0 : z_stage == 1 ? 4 : z_stage == 2 ? 5 : 3;
+  const double cls_bytes = z_stage == 1 ? (double)p->n_pol * 8.0 * in_samples + zrow_bytes
+                           : z_stage == 2 ? 2.0 * zrow_bytes : bytes;
+  ProfScope ps(cls, cls_bytes, s, p->fused || z_stage != 0);
   HIPCHK(pfb::launch_analysis(a, s));
   return PFB_OK;
 }
@@ -736,6 +745,7 @@ struct pfb_synthesis_plan {
   bool deripple = false;
   int chunk_blocks = 0;
   int stage1 = PFB_STAGE1_AUTO;  // pfb_synthesis_set_stage1_rows
+  int last_stage1 = 0;           // pfb_synthesis_last_stage1_rows: where the last launch got its rows
   int rt_chunk_blocks = 64;  // round-trip pipeline chunk (PFB_RT_CHUNK_BLOCKS)
   int timing_mask = 0;  // PFB_TIMING_MASK (timing experiments; results invalid when set)
   int ranges = -1;  // PFB_SYNTH_RANGES: 0 one workgroup per block, -1 persistent auto, >0 persistent
@@ -749,6 +759,7 @@ struct pfb_synthesis_plan {
   DevBuf taper, gainj, sbuf0, sbuf1;  // spectral taper (L), deripple gains (W), scratch
   DevBuf Z, carry, work, stage_in, stage_out;
   int64_t buffered = 0;
+  int64_t ifb_offset = 0;  // InverseFilterBank.sample_offset (0-based; InverseFilterBank.m:12)
   // split round trip: what the analysis half left in Z (analysis plan, n_dat, sample
   // offset, row layout, rows) — the synthesis half must match it; cleared whenever Z is
   // written by anything else
@@ -794,6 +805,9 @@ static int64_t synth_blocks(const pfb_synthesis_plan* p, int64_t n_dat) {
 static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64_t z_ps, int64_t b0,
                                    int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
                                    hipStream_t s, int zblk = 0, const FirSrc* fir = nullptr);
+static pfb::SynthBlockArgs synth_args(const pfb_synthesis_plan* p, const float2* Z, int64_t z_ps,
+                                      int64_t b0, int64_t nb, float2* out, int64_t out_ps,
+                                      int64_t out_limit, int zblk = 0, const FirSrc* fir = nullptr);
 
 // Blocks [b0, b0 + nb) with a spectral taper (pfb_spectral.hip): Matlab's order — per
 // channel FFT, stitch x taper, then the L-point IFFT as row FFTs — in sub-chunks whose
@@ -846,13 +860,16 @@ static pfb_status synthesis_spectral(pfb_synthesis_plan* p, const float2* in, in
 // Blocks [b0, b0 + nb) of a call: channel IFFT of their rows into Z, then the block
 // kernel.  `in` is the call's first channelised row (sample_offset applied).
 // (row_shift: `in` holds the call's channelised rows from row row_shift on — a streaming
-// call whose carried rows are not in front of it; blocks b0.. must not read before it)
+// call whose carried rows are not in front of it; blocks b0.. must not read before it.  A
+// negative row_shift: block 0 starts -row_shift rows into `in` (InverseFilterBank's
+// sample_offset applied to the concatenated rows))
 static pfb_status synthesis_chunk(pfb_synthesis_plan* p, const float2* in, int64_t in_ps, int64_t b0,
                                   int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
                                   hipStream_t s, int64_t row_shift = 0) {
   if (p->has_spectral) {
-    if (row_shift != 0) return fail(PFB_ERR_UNSUPPORTED, "row shift with a spectral taper");
-    return synthesis_spectral(p, in, in_ps, b0, nb, out, out_ps, out_limit, s);
+    // (a negative row shift: the blocks start -row_shift rows into `in` — a sample offset)
+    if (row_shift > 0) return fail(PFB_ERR_UNSUPPORTED, "row shift with a spectral taper");
+    return synthesis_spectral(p, in + (-row_shift) * p->N, in_ps, b0, nb, out, out_ps, out_limit, s);
   }
   const int64_t rows = nb * p->keep + 2 * (int64_t)p->Ov;
   zkey_clear(p);
@@ -873,13 +890,16 @@ static pfb_status synthesis_chunk(pfb_synthesis_plan* p, const float2* in, int64
     ProfScope ps(1, (double)p->n_pol * rows * p->N * 16.0, s);
     HIPCHK(pfb::launch_chan_ifft(c, s));
   }
-  return synthesis_blocks(p, Z, rows * p->N, b0, nb, out, out_ps, out_limit, s);
+  // Z is [row][t0] (run length 1): the Nf = 256 shapes take the wave kernel on it, as the
+  // fused round trip does on its run layout (the block kernel: every other shape)
+  const int zb = pfb::synth_wave_supported(synth_args(p, Z, rows * p->N, b0, nb, out, out_ps, out_limit, 1)) ? 1 : 0;
+  return synthesis_blocks(p, Z, rows * p->N, b0, nb, out, out_ps, out_limit, s, zb);
 }
 
 // Block kernel over blocks [b0, b0 + nb); Z row 0 is channelised row b0 * keep.
 static pfb::SynthBlockArgs synth_args(const pfb_synthesis_plan* p, const float2* Z, int64_t z_ps,
                                       int64_t b0, int64_t nb, float2* out, int64_t out_ps,
-                                      int64_t out_limit, int zblk = 0, const FirSrc* fir = nullptr) {
+                                      int64_t out_limit, int zblk, const FirSrc* fir) {
   pfb::SynthBlockArgs a{};
   if (fir) {
     a.fir_x = fir->x;
@@ -928,6 +948,7 @@ static pfb_status synthesis_blocks(pfb_synthesis_plan* p, const float2* Z, int64
                                    int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
                                    hipStream_t s, int zblk, const FirSrc* fir) {
   const pfb::SynthBlockArgs a = synth_args(p, Z, z_ps, b0, nb, out, out_ps, out_limit, zblk, fir);
+  p->last_stage1 = fir ? PFB_STAGE1_RECOMPUTED : PFB_STAGE1_STORED;
   {
     ProfScope ps(2, (double)p->n_pol * (nb * p->keep * p->N * 8.0 + nb * p->Lkeep * 8.0), s);
     HIPCHK(pfb::launch_synth_block(a, s));
@@ -1219,6 +1240,8 @@ pfb_status pfb_synthesis_set_stage1_rows(pfb_synthesis_plan* p, int32_t mode) {
   return PFB_OK;
 }
 
+int32_t pfb_synthesis_last_stage1_rows(const pfb_synthesis_plan* p) { return p ? p->last_stage1 : -1; }
+
 pfb_status pfb_synthesis_set_chunk_blocks(pfb_synthesis_plan* p, int32_t blocks) {
   if (!p) return fail(PFB_ERR_INVALID_ARG, "null plan");
   p->chunk_blocks = std::max(0, blocks);
@@ -1259,48 +1282,65 @@ pfb_status pfb_synthesis_execute(pfb_synthesis_plan* p, const pfb_cf32* in, int6
   return PFB_OK;
 }
 
+pfb_status pfb_inverse_filterbank_set_sample_offset(pfb_synthesis_plan* p, int64_t sample_offset) {
+  if (!p) return fail(PFB_ERR_INVALID_ARG, "null plan");
+  if (sample_offset < 0) return fail(PFB_ERR_INVALID_ARG, "sample_offset is 0-based (>= 0)");
+  p->ifb_offset = sample_offset;
+  return PFB_OK;
+}
+
+// InverseFilterBank.m:73-135.  Every call runs polyphase_synthesis on the concatenated
+// rows (carry + input) from row `so` = sample_offset on (:92-96, `sample_offset+1`), and the
+// carry starts at input_idat = (output length) nu / (n_chan de) = B keep of the
+// concatenation — not offset by `so`: the next call skips `so` rows of it again, so
+// consecutive calls see the blocks of one continuous run.
 pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* p, const pfb_cf32* in, int64_t in_ps,
                                           int64_t n_in, pfb_cf32* out, int64_t out_ps, int64_t cap,
                                           int64_t* n_out, int32_t mem, void* stream) {
   if (!p || (!in && n_in > 0)) return fail(PFB_ERR_INVALID_ARG, "null argument");
+  if (n_in < 0) return fail(PFB_ERR_INVALID_ARG, "negative n_in");
   HIPCHK(hipSetDevice(p->device));
   hipStream_t s = (hipStream_t)stream;
   const int N = p->N;
   const int64_t total = p->buffered + n_in;
   const hipMemcpyKind kin = mem == PFB_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  const int64_t so = std::min(p->ifb_offset, total);  // in(:, :, sample_offset:end)
+  // output length and carry-over rounded up to a multiple of nu (InverseFilterBank.m:104-135)
+  const int64_t B = synth_blocks(p, total - so);
+  const int64_t full = B * p->Lkeep;
+  int64_t input_idat = B * p->keep;
+  int64_t buffered = total - input_idat;
+  int64_t olen = full;
+  const int64_t rem = ((buffered % p->nu) + p->nu) % p->nu;
+  if (rem != 0) {
+    buffered += p->nu - rem;
+    input_idat = total - buffered;
+    // output_ndat = input_idat * (n_chan de)/nu, used as a Matlab colon end (floor)
+    olen = std::min(std::max<int64_t>(0, floordiv(input_idat * N * p->de, p->nu)), full);
+  }
+  if (input_idat < 0)
+    // no complete block and a carry rounded up past the data: InverseFilterBank.m:104-122
+    // would index input(:, :, input_idat + 1 : end) before the first sample (its rounding
+    // loop never settles); the call is rejected and the object state is left unchanged
+    return fail(PFB_ERR_INVALID_ARG,
+                "InverseFilterBank: %lld buffered + %lld new rows hold no complete block and "
+                "round the carry past the data (InverseFilterBank.m:104-122); pass more rows",
+                (long long)p->buffered, (long long)n_in);
+  if (n_out) *n_out = olen;
+  if (olen > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld",
+                              (long long)cap, (long long)olen);
   {
     // Carry without the concatenation copy: blocks whose rows start at or after the
-    // carried Bc rows read the new input in place (row shift Bc), the first ceil(Bc / keep)
-    // blocks a small stitched buffer; same blocks, same kernels as the concatenated run.
+    // carried Bc rows read the new input in place (row shift Bc - so), the first ones a
+    // small stitched buffer; same blocks, same kernels as the concatenated run.
     const int64_t Bc = p->buffered;
-    const int64_t B = synth_blocks(p, total);
-    const int64_t full = B * p->Lkeep;
-    int64_t input_idat = B * p->keep;
-    int64_t buffered = total - input_idat;
-    int64_t olen = full;
-    const int64_t rem = ((buffered % p->nu) + p->nu) % p->nu;
-    if (rem != 0) {
-      buffered += p->nu - rem;
-      input_idat = total - buffered;
-      olen = std::min(std::max<int64_t>(0, floordiv(input_idat * N * p->de, p->nu)), full);
-    }
-    if (input_idat < 0)
-      // no complete block and a carry rounded up past the data: InverseFilterBank.m:104-122
-      // would index input(:, :, input_idat + 1 : end) before the first sample (its rounding
-      // loop never settles); the call is rejected and the object state is left unchanged
-      return fail(PFB_ERR_INVALID_ARG,
-                  "InverseFilterBank: %lld buffered + %lld new rows hold no complete block and "
-                  "round the carry past the data (InverseFilterBank.m:104-122); pass more rows",
-                  (long long)Bc, (long long)n_in);
     static const bool no_split = pfb::knob("PFB_FB_NO_SPLIT") != nullptr;  // A/B
     if (!no_split && mem == PFB_MEM_DEVICE && Bc > 0 && !p->has_spectral && input_idat >= Bc) {
-      if (n_out) *n_out = olen;
-      if (olen > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld",
-                                  (long long)cap, (long long)olen);
       if (olen > 0) {
-        const int64_t b_s = std::min(B, (Bc + p->keep - 1) / p->keep);
+        // first block starting at or after row Bc of the concatenation: so + b keep >= Bc
+        const int64_t b_s = std::min(B, std::max<int64_t>(0, (Bc - so + p->keep - 1) / p->keep));
         if (b_s > 0) {
-          const int64_t L = std::min(total, (b_s - 1) * p->keep + p->Nf);
+          const int64_t L = std::min(total, so + (b_s - 1) * p->keep + p->Nf);
           HIPCHK(p->work.ensure((size_t)p->n_pol * L * N * sizeof(float2)));
           float2* wk = p->work.as<float2>();
           HIPCHK(copy_pols(wk, L * N, p->carry.as<float2>(), Bc * N, std::min(Bc, L) * N, p->n_pol,
@@ -1308,10 +1348,11 @@ pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* p, const pfb_cf32*
           if (L > Bc)
             HIPCHK(copy_pols(wk + Bc * N, L * N, (const float2*)in, in_ps, (L - Bc) * N, p->n_pol,
                              hipMemcpyDeviceToDevice, s));
-          pfb_status st = synthesis_range(p, wk, L * N, 0, b_s, (float2*)out, out_ps, olen, s);
+          pfb_status st = synthesis_range(p, wk, L * N, 0, b_s, (float2*)out, out_ps, olen, s, -so);
           if (st != PFB_OK) return st;
         }
-        pfb_status st = synthesis_range(p, (const float2*)in, in_ps, b_s, B, (float2*)out, out_ps, olen, s, Bc);
+        pfb_status st =
+            synthesis_range(p, (const float2*)in, in_ps, b_s, B, (float2*)out, out_ps, olen, s, Bc - so);
         if (st != PFB_OK) return st;
       }
       if (buffered > 0) {
@@ -1339,32 +1380,15 @@ pfb_status pfb_inverse_filterbank_execute(pfb_synthesis_plan* p, const pfb_cf32*
     w = wk;
     wps = total * N;
   }
-  // output length and carry-over rounded up to a multiple of nu (InverseFilterBank.m:104-135)
-  const int64_t B = synth_blocks(p, total);
-  const int64_t full = B * p->Lkeep;
-  int64_t input_idat = B * p->keep;
-  int64_t buffered = total - input_idat;
-  int64_t olen = full;
-  const int64_t rem = ((buffered % p->nu) + p->nu) % p->nu;
-  if (rem != 0) {
-    buffered += p->nu - rem;
-    input_idat = total - buffered;
-    // output_ndat = input_idat * (n_chan de)/nu, used as a Matlab colon end (floor)
-    olen = std::max<int64_t>(0, floordiv(input_idat * N * p->de, p->nu));
-    olen = std::min(olen, full);
-  }
-  if (n_out) *n_out = olen;
-  if (olen > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld",
-                              (long long)cap, (long long)olen);
   if (olen > 0) {
     if (mem == PFB_MEM_HOST) {
       HIPCHK(p->stage_out.ensure((size_t)p->n_pol * olen * sizeof(float2)));
-      pfb_status st = synthesis_run(p, w, wps, total, p->stage_out.as<float2>(), olen, olen, s);
+      pfb_status st = synthesis_range(p, w, wps, 0, B, p->stage_out.as<float2>(), olen, olen, s, -so);
       if (st != PFB_OK) return st;
       HIPCHK(copy_pols((float2*)out, out_ps, p->stage_out.as<float2>(), olen, olen, p->n_pol,
                        hipMemcpyDeviceToHost, s));
     } else {
-      pfb_status st = synthesis_run(p, w, wps, total, (float2*)out, out_ps, olen, s);
+      pfb_status st = synthesis_range(p, w, wps, 0, B, (float2*)out, out_ps, olen, s, -so);
       if (st != PFB_OK) return st;
     }
   }
@@ -1610,8 +1634,18 @@ static pfb_status roundtrip_run(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, c
       return PFB_OK;
     }
     if (C <= 1 || !zblk) {
-      pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0,
-                                   nullptr, zblk);
+      // (generic N > 256 path: the FIR and the row FFT as two calls on the stream — the same
+      // two launches as one call, each then timed alone by the profiler)
+      pfb_status st = PFB_OK;
+      if (!pa->fused) {
+        st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0, nullptr, zblk,
+                          nullptr, 1);
+        if (st == PFB_OK)
+          st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0, nullptr, zblk,
+                            nullptr, 2);
+      } else {
+        st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0, nullptr, zblk);
+      }
       if (st != PFB_OK) return st;
       return synthesis_blocks(ps, Z + (off - z0) * pa->N, zrows * pa->N, 0, B, (float2*)out, out_ps,
                               olen, s, zblk);
@@ -1752,7 +1786,7 @@ pfb_status pfb_profile_enable(int32_t enable) {
   return PFB_OK;
 }
 pfb_status pfb_profile_read(int32_t which, double* total_ms, int64_t* launches, double* bytes) {
-  if (which < 0 || which > 3) return fail(PFB_ERR_INVALID_ARG, "which must be 0..3");
+  if (which < 0 || which >= Profiler::kClasses) return fail(PFB_ERR_INVALID_ARG, "which must be 0..5");
   g_prof.drain();
   if (total_ms) *total_ms = g_prof.total_ms[which];
   if (launches) *launches = g_prof.launches[which];
@@ -1761,7 +1795,7 @@ pfb_status pfb_profile_read(int32_t which, double* total_ms, int64_t* launches, 
 }
 pfb_status pfb_profile_reset(void) {
   g_prof.drain();
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < Profiler::kClasses; ++i) {
     g_prof.total_ms[i] = 0;
     g_prof.launches[i] = 0;
     g_prof.bytes[i] = 0;
@@ -1770,7 +1804,7 @@ pfb_status pfb_profile_reset(void) {
   return PFB_OK;
 }
 pfb_status pfb_profile_kernel_name(int32_t which, char* buf, int64_t len) {
-  if (which < 0 || which > 3) return fail(PFB_ERR_INVALID_ARG, "which must be 0..3");
+  if (which < 0 || which >= Profiler::kClasses) return fail(PFB_ERR_INVALID_ARG, "which must be 0..5");
   if (!buf || len <= 0) return fail(PFB_ERR_INVALID_ARG, "null or empty buffer");
   const std::string& n = g_prof.names[which];
   const size_t k = std::min<size_t>(n.size(), (size_t)len - 1);

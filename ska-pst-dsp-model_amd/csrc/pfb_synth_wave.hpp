@@ -318,8 +318,8 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     });
     if constexpr (PRIO & 25) __builtin_amdgcn_s_setprio(0);
     if constexpr (XW) __syncthreads();  // the phase tiles were written by every wave
-    if constexpr (PRIO & 4) __builtin_amdgcn_s_setprio(2);
     else __builtin_amdgcn_wave_barrier();
+    if constexpr (PRIO & 4) __builtin_amdgcn_s_setprio(2);
     static_for<0, 8>([&](auto k) {
       lds_pair(lds + rd1 + 16 * k, v[2 * k], v[2 * k + 1]);
     });

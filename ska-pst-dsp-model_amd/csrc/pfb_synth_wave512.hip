@@ -20,7 +20,9 @@
 //            registers, x w_28^{+g t'}, radix-2 across the lane pair -> lane e holds
 //            t1a = t' + 14 e; x e^{+2 pi i f1 t1a / W}
 //   swap 2   (t1a, phase) <- Y_f1[t1a], f1 < 16, across the workgroup
-//   pass B   16-point IDFT over f1          -> y[t1a + 28 t1b], stored when t1 is kept.
+//   pass B   16-point IDFT over f1          -> y[t1a + 28 t1b]; the kept outputs t1 in
+//            [L_ov / N, W - L_ov / N) = [112, 336) are exactly t1b in [4, 12), so only those
+//            8 of the 16 outputs are formed and stored.
 // Both lane-pair butterflies compute self + sigma * partner in one fma per float (sigma = -1
 // on the second lane of the pair); the sign that leaves on that lane's result is folded
 // into its next twiddle table row, so no lane needs a select.
@@ -29,6 +31,12 @@
 // and output line).  Every twiddle is a table entry rounded once from double; the gain x
 // twiddle x scale constants come from the plan's tw4s table, once per launch.
 // Register budget: 3 waves per SIMD (<= 168 VGPRs); LDS 47 KB per workgroup (3 per CU).
+// LDS layout (scripts/lds_bank_model.py; round 5): every swap access is bank-conflict-free —
+// phase tiles 4624 B apart (1156 dwords: the 8 tiles of a swap-1 ds_write_b64 group on
+// distinct 16-B bank quads), swap-1 rows [f1][h] 288 / 144 B apart, swap-2 row t1a at slot
+// kSw2Row[t1a] (rows of 144 B): a ds_write_b64 group's two lane halves (e = 0 / 1) 576 B
+// apart and each pass-B ds_read_b128 group's 4 rows x 4 phases on 16 distinct 16-B units
+// (round 4: 37.6 % of the LDS cycles were bank conflicts, the model gives the same figure).
 #include "pfb_common.hpp"
 
 namespace pfb {
@@ -38,9 +46,25 @@ namespace {
 constexpr int kW5Threads = 256;
 constexpr int kW5Cols = 8;       // output phases per workgroup
 constexpr int kRowB = 144;       // 16 values + 16 B
-constexpr int kTileB = 2 * 16 * kRowB + 32;  // one phase: swap 1 [f1][h][l'] (f1 stride 288 B),
-                                             // swap 2 rows of 144 B (28 rows); the 32 B
-                                             // put the 8 tiles on different banks
+constexpr int kTileB = 2 * 16 * kRowB + 16;  // one phase: swap 1 [f1][h][l'] (f1 stride 288 B),
+                                             // swap 2 row slots of 144 B (32 slots, 28 used)
+// swap-2 row slot of t1a = t' + 14 e: sw2_slot(t') + 4 e (slots s with 9 s mod 16 in the
+// pattern the pass-B read groups need, lds_bank_model.py)
+constexpr int sw2_slot(int t) {
+  constexpr int s[14] = {0, 16, 8, 24, 9, 25, 1, 2, 18, 10, 26, 11, 27, 3};
+  return s[t];
+}
+// the same for a run-time t (< 28), from two packed constants (5 bits per slot)
+constexpr uint64_t sw2_pack(int t0) {
+  uint64_t v = 0;
+  for (int i = 0; i < 7; ++i) v |= (uint64_t)sw2_slot(t0 + i) << (5 * i);
+  return v;
+}
+__device__ __forceinline__ int sw2_slot_rt(int t1a) {
+  const int tp = t1a % 14;
+  const uint64_t pk = tp < 7 ? sw2_pack(0) : sw2_pack(7);
+  return (int)((pk >> (5 * (tp % 7))) & 31u) + 4 * (t1a / 14);
+}
 constexpr int kTw1Off = kW5Cols * kTileB;          // [m][f1], 32 rows
 constexpr int kTw32Off = kTw1Off + 32 * kRowB;     // [h][f2'], 2 rows
 constexpr int kRow14B = 112;                       // 14 values
@@ -74,6 +98,28 @@ __device__ __forceinline__ void twiddle_rows(float2* v, const char* row) {
     lds_pair2(row + 16 * k, w0, w1);
     v[2 * k] = cmul(v[2 * k], w0);
     v[2 * k + 1] = cmul(v[2 * k + 1], w1);
+  });
+}
+
+// y[j] = sum_f v[f] e^{+2 pi i f (4 + j) / 16}, j < 8: outputs 4 .. 11 of the 16-point
+// inverse DFT — sdft<16, +1>'s 4 x 4 split (output k1 + 4 k2) with only k2 = 1, 2 formed
+__device__ __forceinline__ void idft16_mid8(const float2* v, float2* y) {
+  float2 t[4][4];
+  static_for<0, 4>([&](auto n1) {
+    constexpr int a1 = decltype(n1)::value;
+    static_for<0, 4>([&](auto n2) { t[a1][decltype(n2)::value] = v[4 * decltype(n2)::value + a1]; });
+    sdft<4, +1>(t[a1]);
+    static_for<1, 4>([&](auto k1) {
+      t[a1][decltype(k1)::value] = ctw<a1 * decltype(k1)::value, 16, +1>(t[a1][decltype(k1)::value]);
+    });
+  });
+  static_for<0, 4>([&](auto k1) {
+    constexpr int c1 = decltype(k1)::value;
+    // X[1] = (z0 - z2) + i (z1 - z3), X[2] = (z0 + z2) - (z1 + z3) of z[n1] = t[n1][k1]
+    const float2 d02 = csub(t[0][c1], t[2][c1]), s02 = cadd(t[0][c1], t[2][c1]);
+    const float2 d13 = crot90<+1>(csub(t[1][c1], t[3][c1])), s13 = cadd(t[1][c1], t[3][c1]);
+    y[c1] = cadd(d02, d13);       // t1b = 4 + k1
+    y[4 + c1] = csub(s02, s13);   // t1b = 8 + k1
   });
 }
 
@@ -158,12 +204,11 @@ void synth_wave512_kernel(SynthBlockArgs a) {
 
   const int wr1 = c1 * kTileB + (m >> 4) * kRowB + (m & 15) * 8;  // swap-1 writes (+ f1 * 288)
   const int rd1 = tile + f1 * (2 * kRowB) + h * kRowB;     // swap-1 reads (+ 16 k)
-  const int wr2 = tile + h * kRowB + f1 * 8;               // swap-2 writes (+ t' * 288)
-  // swap 2 keeps row t1a = t' + 14 e at row 2 t' + e (the two lanes of a pair write
-  // neighbouring rows: fewer bank conflicts than rows t' and t' + 14)
+  const int wr2 = tile + h * (4 * kRowB) + f1 * 8;         // swap-2 writes (+ sw2_slot(t') * 144)
   const int col2 = lane & 7;
   const int t1a = (lane >> 3) < 7 ? 7 * wave + (lane >> 3) : 28;  // 28: no output (8 lanes a wave)
-  const int rd2 = col2 * kTileB + (t1a < 28 ? 2 * (t1a % 14) + t1a / 14 : 0) * kRowB;  // (+ 16 k)
+  // (the idle lanes read the row of t1a = 7 wave + 6: a slot their read groups leave free)
+  const int rd2 = col2 * kTileB + sw2_slot_rt(t1a < 28 ? t1a : 7 * wave + 6) * kRowB;  // (+ 16 k)
   const char* tw1row = lds + kTw1Off + m * kRowB;
   const char* tw32row = lds + kTw32Off + h * kRowB;
   const char* w28row = lds + kW28Off + h * kRow14B;
@@ -250,25 +295,25 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     // own swap-1 reads of the tile are issued before these writes)
     __builtin_amdgcn_wave_barrier();
     static_for<0, 14>([&](auto t) {
-      *reinterpret_cast<float2*>(lds + wr2 + decltype(t)::value * (2 * kRowB)) = u[decltype(t)::value];
+      *reinterpret_cast<float2*>(lds + wr2 + sw2_slot(decltype(t)::value) * kRowB) = u[decltype(t)::value];
     });
     __syncthreads();
     static_for<0, 8>([&](auto k) { lds_pair2(lds + rd2 + 16 * k, v[2 * k], v[2 * k + 1]); });
-    // ---- pass B: 16-point IDFT over f1 -> t1 = t1a + 28 t1b; overlap-discard on the store
-    sdft<16, +1>(v);
+    // ---- pass B: 16-point IDFT over f1 -> t1 = t1a + 28 t1b, only t1b in [4, 12) (the kept
+    // outputs: L_ov = 112 N); stored as output sample (t1a + 28 (t1b - 4)) N + t0
+    float2 y[8];
+    idft16_mid8(v, y);
     {
       const int64_t ob = (a.block0 + b) * (int64_t)a.Lkeep;  // first kept output sample
       const int64_t avail = a.out_limit - ob;
       const int64_t nk = (tmask(a.timing_mask) & 2)
                              ? 0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
       const __amdgpu_buffer_rsrc_t o = make_rsrc(opol + ob, (uint32_t)nk * 8u);
-      // lanes t1a >= 28 hold no output: their offsets leave the descriptor's range (as do
-      // the discarded t1 < t1_lo, whose negative offsets wrap past 2^31)
-      int base = (t1a < 28) ? (t1a * N - a.Lov + t0g + col2) * 8 : (int)0x80000000;
-      // (recomputed every block: 16 hoisted store offsets would not fit the register budget)
+      // lanes t1a >= 28 hold no output: their offsets leave the descriptor's range
+      int base = (t1a < 28) ? (t1a * N + t0g + col2) * 8 : (int)0x80000000;
       asm volatile("" : "+v"(base));
-      static_for<0, 16>([&](auto t) {
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v[t]), o,
+      static_for<0, 8>([&](auto t) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y[t]), o,
                                               (uint32_t)(base + t * 28 * N * 8), 0, kNtW5 ? 2 : 0);
       });
     }
@@ -277,8 +322,9 @@ void synth_wave512_kernel(SynthBlockArgs a) {
 
 bool synth_wave512_supported(const SynthBlockArgs& a) {
   // (32-bit byte offsets: 512 rows x N phases x 8 B per block stay below 2^31)
+  // (L_ov = 112 N: pass B forms and stores only t1b in [4, 12))
   return a.Nf == 512 && a.W == 448 && a.keep == 256 && a.zblk <= 1 && a.N % kW5Cols == 0 &&
-         a.N <= 65536 && a.tw4s != nullptr;
+         a.N <= 65536 && a.tw4s != nullptr && a.Lov == 112 * a.N;
 }
 
 template <bool SPANS, bool XW, bool WFLAT = false>

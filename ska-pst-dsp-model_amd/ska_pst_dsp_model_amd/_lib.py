@@ -98,8 +98,10 @@ SYMBOLS = [
                                                  c_void_p]),
     ("pfb_inverse_filterbank_buffered", c_int64, [c_void_p]),
     ("pfb_inverse_filterbank_reset", c_int32, [c_void_p]),
+    ("pfb_inverse_filterbank_set_sample_offset", c_int32, [c_void_p, c_int64]),
     ("pfb_synthesis_set_chunk_blocks", c_int32, [c_void_p, c_int32]),
     ("pfb_synthesis_set_stage1_rows", c_int32, [c_void_p, c_int32]),
+    ("pfb_synthesis_last_stage1_rows", c_int32, [c_void_p]),
     ("pfb_roundtrip_execute", c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                         c_void_p, c_int64, c_int64, POINTER(c_int64), c_int64,
                                         c_void_p, c_int64, c_int64, POINTER(c_int64), c_void_p]),

@@ -327,6 +327,14 @@ class SynthesisPlan:
         synthesis evaluates them from the input series (N = 256 streaming shapes;
         bit-identical output); 'auto' — the measured-faster one."""
         _lib.check(self._lib.pfb_synthesis_set_stage1_rows(self._h, self.STAGE1_ROWS[mode]))
+        self._rt_input = None  # a split round trip in flight is not continued under another mode
+
+    @property
+    def last_stage1_rows(self) -> str:
+        """Where the plan's last synthesis launch got its stage-1 rows ('stored',
+        'recomputed'; 'none' before any launch) — pfb_synthesis_last_stage1_rows."""
+        m = int(self._lib.pfb_synthesis_last_stage1_rows(self._h))
+        return {_lib.PFB_STAGE1_STORED: "stored", _lib.PFB_STAGE1_RECOMPUTED: "recomputed"}.get(m, "none")
 
     def output_length(self, n_dat: int) -> int:
         return int(self._lib.pfb_synthesis_output_length(self._h, int(n_dat)))
@@ -337,6 +345,11 @@ class SynthesisPlan:
 
     def reset(self):
         _lib.check(self._lib.pfb_inverse_filterbank_reset(self._h))
+
+    def set_stream_sample_offset(self, sample_offset: int):
+        """InverseFilterBank.sample_offset (0-based) of the stateful ``execute(...,
+        stateful=True)`` calls (pfb_inverse_filterbank_set_sample_offset)."""
+        _lib.check(self._lib.pfb_inverse_filterbank_set_sample_offset(self._h, int(sample_offset)))
 
     def _prep_in(self, x, layout: str):
         """Accept (n_pol, n_chan, n_dat) Matlab-shaped or (n_pol, n_dat, n_chan) buffers."""
@@ -444,6 +457,10 @@ def roundtrip_analysis(analysis: AnalysisPlan, synthesis: SynthesisPlan, x, samp
         analysis._h, synthesis._h, c_void_p(x.data_ptr()), n_dat, n_dat,
         c_void_p(chan.data_ptr()), K * analysis.n_chan, K, byref(kr), int(sample_offset),
         _stream_of(x, analysis, synthesis)))
+    # with recomputed stage-1 rows the synthesis half re-reads this input: `x` may be a
+    # temporary made by _prep_in (another dtype, a non-contiguous view), so the plan keeps
+    # it alive until roundtrip_synthesis has been enqueued (which records it on its stream)
+    synthesis._rt_input = x
     return chan
 
 
@@ -463,9 +480,17 @@ def roundtrip_synthesis(analysis: AnalysisPlan, synthesis: SynthesisPlan, n_dat:
     if tuple(out.shape) != (n_pol, n_out):
         raise ValueError("preallocated out has the wrong shape")
     no = c_int64(0)
+    stream = _stream_of(out, analysis, synthesis)
     _lib.check(_lib.load().pfb_roundtrip_synthesis_execute(
         analysis._h, synthesis._h, int(n_dat), int(sample_offset), c_void_p(out.data_ptr()),
-        max(n_out, 1), n_out, byref(no), _stream_of(out, analysis, synthesis)))
+        max(n_out, 1), n_out, byref(no), stream))
+    xin = getattr(synthesis, "_rt_input", None)
+    if xin is not None:
+        # the analysis half's input (recomputed rows read it here): its memory may be reused
+        # only after the work just enqueued on this stream has finished
+        if not t.cuda.is_current_stream_capturing():
+            xin.record_stream(t.cuda.current_stream(out.device))
+        synthesis._rt_input = None
     return out
 
 

@@ -192,9 +192,11 @@ class InverseFilterBank(DeChannelizer):
         shape = tuple(input.shape)
         if not is_device_array(input) and not np.iscomplexobj(np.asarray(input)):
             raise ValueError("polyphase_synthesis input data are real-valued!")
-        if self.sample_offset != 0:
-            raise NotImplementedError("stateful synthesis with sample_offset != 0")
+        if int(self.sample_offset) < 0:
+            raise ValueError("sample_offset is 0-based (>= 0)")
         plan = self._ensure_plan(shape[0], shape[1])
+        # polyphase_synthesis(..., obj.sample_offset+1, ...) on every call (:92-96)
+        plan.set_stream_sample_offset(int(self.sample_offset))
         out = plan.execute(input, stateful=True)
         return self, out[:, None, :]
 

@@ -506,6 +506,47 @@ def test_inverse_filterbank_stream_carry_in_place(gpu, N, nf, ov, chunks):
         assert ifb.buffered_samples == oifb.buffered_samples
 
 
+@pytest.mark.parametrize("N,nf,ov,so,chunks,device", [
+    (8, 128, 16, 5, (500, 333, 1000, 20, 777), False),
+    (8, 128, 16, 37, (300, 2000, 96, 1234), True),
+    (8, 128, 16, 200, (150, 700, 2100), True),          # offset longer than a block
+    (256, 256, 48, 17, (1000, 161, 5000, 3, 2222), True),
+])
+def test_inverse_filterbank_sample_offset_matches_oracle(gpu, N, nf, ov, so, chunks, device):
+    """InverseFilterBank.sample_offset != 0 (InverseFilterBank.m:12,92-96): every call
+    synthesises the concatenated carry + input from row sample_offset on, and the carry
+    starts at the consumed blocks' end (:104-133) — against InverseFilterBankOracle (its
+    literal restatement) over several chunkings, host and device inputs, with the carry
+    in place (row shift) and stitched."""
+    import torch
+    pfb = _pfb()
+    taps = _taps("test") if N == 8 else _taps("low87")
+    cfg = dict(filt_coeff=taps, channels=N, os_factor="8/7", input_fft_length=nf,
+               input_overlap=ov, deripple=True, temporal_taper="tukey")
+    ifb = pfb.InverseFilterBank(cfg)
+    ifb.sample_offset = so
+    oifb = orc.InverseFilterBankOracle(taps, N, "8/7", nf, ov, "tukey", deripple=True, sample_offset=so)
+    rng = np.random.default_rng(45 + so)
+    produced = 0
+    for n in chunks:
+        x = _noise(rng, (2, N, n))
+        xin = torch.from_numpy(x).to(gpu) if device else x
+        try:
+            ref = oifb.execute(x)
+        except ValueError:
+            with pytest.raises(pfb.PfbError):
+                ifb.execute(xin)
+            continue
+        ifb, got = ifb.execute(xin)
+        got = got.cpu().numpy() if hasattr(got, "cpu") else np.asarray(got)
+        assert got.shape == ref.shape, (n, got.shape, ref.shape)
+        if ref.size:
+            assert_pfb_close(got, ref, what=f"inverse stream offset {so} N={N} chunk {n}")
+        produced += ref.shape[2]
+        assert ifb.buffered_samples == oifb.buffered_samples
+    assert produced > 0
+
+
 # ----------------------------------------------------------------------------- spectral taper
 # polyphase_synthesis.m:282 (FFFF = spectral_taper(FFFF, L, Ov)) through
 # InverseFilterBank.frequency_taper (InverseFilterBank.m:48-61); 'hann' on the L-vector

@@ -650,9 +650,13 @@ def test_roundtrip_recomputed_stage1_rows_bit_identical(gpu, os_, tpc, n, so, n_
         return a, s
     a0, s0 = pair("stored")
     c_ref, o_ref = pfb.roundtrip(a0, s0, x, sample_offset=so)
+    assert s0.last_stage1_rows == "stored"
     a1, s1 = pair("recomputed")
     c1, o1 = pfb.roundtrip(a1, s1, x, sample_offset=so)
     torch.cuda.synchronize()
+    # the recomputing kernel ran (not a silent fall-back to stored rows, which would give
+    # the same bits)
+    assert s1.last_stage1_rows == "recomputed"
     assert torch.equal(c1, c_ref)
     assert torch.equal(o1, o_ref)
     # split halves on two streams
@@ -662,6 +666,7 @@ def test_roundtrip_recomputed_stage1_rows_bit_identical(gpu, os_, tpc, n, so, n_
     with torch.cuda.stream(ss):
         out = pfb.roundtrip_synthesis(a1, s1, x.shape[1], sample_offset=so, device=gpu.index or 0)
     torch.cuda.synchronize()
+    assert s1.last_stage1_rows == "recomputed"
     assert torch.equal(chan, c_ref)
     assert torch.equal(out, o_ref)
     # the analysis half of one mode is not continued by the other
@@ -694,4 +699,40 @@ def test_roundtrip_recomputed_rows_reject_mismatch(gpu):
     out = pfb.roundtrip_synthesis(a, s, x.shape[1], device=dev)
     _, o_ref = pfb.roundtrip(b, s, x)
     torch.cuda.synchronize()
+    assert torch.equal(out, o_ref)
+
+
+@pytest.mark.parametrize("kind", ["complex128", "strided"])
+def test_roundtrip_recomputed_split_temporary_input(gpu, kind):
+    """Split round trip with recomputed stage-1 rows whose input is NOT a contiguous
+    complex64 tensor: _prep_in makes a temporary, which the synthesis half re-reads after
+    roundtrip_analysis has returned.  The plan keeps it alive until roundtrip_synthesis has
+    been enqueued (and records it on that stream), so allocations in between — which the
+    caching allocator would serve from a freed temporary — cannot overwrite it."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
+    win = pfb.PFBWindow().lookup["tukey"](256, 48)
+    n = 1 << 20
+    x64 = _noise_t(torch, gpu, (1, n), 41)
+    if kind == "complex128":
+        xin = x64.to(torch.complex128)
+    else:
+        big = torch.zeros((1, 2 * n), dtype=torch.complex64, device=gpu)
+        big[:, ::2] = x64
+        xin = big[:, ::2]
+        assert not xin.is_contiguous()
+    a0 = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
+    s0 = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, 1, 0)
+    _, o_ref = pfb.roundtrip(a0, s0, x64)
+    a1 = pfb.AnalysisPlan(taps, 256, "8/7", "polyphase_analysis", 1, 0)
+    s1 = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, 1, 0)
+    s1.set_stage1_rows("recomputed")
+    pfb.roundtrip_analysis(a1, s1, xin)
+    # allocations of the temporary's size, filled with garbage, on the same stream
+    junk = [torch.full((1, n), 7.0 + 3.0j, dtype=torch.complex64, device=gpu) for _ in range(4)]
+    out = pfb.roundtrip_synthesis(a1, s1, n, device=gpu.index or 0)
+    torch.cuda.synchronize()
+    del junk
+    assert s1.last_stage1_rows == "recomputed"
     assert torch.equal(out, o_ref)
