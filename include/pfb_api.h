@@ -93,6 +93,9 @@ typedef struct pfb_analysis_plan pfb_analysis_plan;
 /* Replaces: FilterBank constructor (FilterBank.m:26-63) + read_fir_filter_coeff. */
 pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* desc, pfb_analysis_plan** plan);
 pfb_status pfb_analysis_plan_destroy(pfb_analysis_plan* plan);
+/* The checks and host-side tables of pfb_analysis_plan_create without a device (nothing
+ * allocated, nothing kept): the status create would return before touching the GPU. */
+pfb_status pfb_analysis_plan_validate(const pfb_analysis_desc* desc);
 
 /* Number of output samples per channel for n_dat input samples of a stateless call:
  * Bunton K = floor((n_dat - P*N)/M) (polyphase_analysis.m:62), padded K = floor(n_dat/M)
@@ -171,6 +174,10 @@ typedef struct pfb_synthesis_plan pfb_synthesis_plan;
  * PFBWindow lookup and the freqz-based deripple response (polyphase_synthesis.m:138-150). */
 pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* desc, pfb_synthesis_plan** plan);
 pfb_status pfb_synthesis_plan_destroy(pfb_synthesis_plan* plan);
+/* The checks and host-side tables (window, deripple gains, four-step twiddles) of
+ * pfb_synthesis_plan_create without a device: the status create would return before
+ * touching the GPU. */
+pfb_status pfb_synthesis_plan_validate(const pfb_synthesis_desc* desc);
 
 /* n_blocks * output_keep for n_dat channelised samples (polyphase_synthesis.m:112-131). */
 int64_t pfb_synthesis_output_length(const pfb_synthesis_plan* plan, int64_t n_dat);

@@ -397,9 +397,10 @@ int32_t pfb_device_count(void) {
   return n;
 }
 
-pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_plan** out) {
-  if (!d || !out) return fail(PFB_ERR_INVALID_ARG, "null argument");
-  *out = nullptr;
+// Descriptor checks of pfb_analysis_plan_create (no device needed); fills the plan's
+// scalar parameters into `p`
+static pfb_status analysis_validate(const pfb_analysis_desc* d, pfb_analysis_plan* p) {
+  if (!d) return fail(PFB_ERR_INVALID_ARG, "null argument");
   if (d->variant == PFB_ANALYSIS_LOWCBF &&
       (d->n_chan != 256 || d->os_nu != 4 || d->os_de != 3 || d->n_taps != 3072))
     return fail(PFB_ERR_INVALID_ARG,
@@ -416,15 +417,11 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
   if (d->n_pol <= 0) return fail(PFB_ERR_INVALID_ARG, "n_pol must be positive");
   if (d->n_pol > 65535)  // polarisations map to grid.y of every launch
     return fail(PFB_ERR_INVALID_ARG, "n_pol = %d exceeds 65535 series per plan", d->n_pol);
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
-    return fail(PFB_ERR_NO_DEVICE, "no HIP device available");
-  if (d->device < 0 || d->device >= ndev)
-    return fail(PFB_ERR_INVALID_ARG, "device %d out of range (%d devices)", d->device, ndev);
-  static std::atomic<uint64_t> next_serial{1};
-  auto* p = new pfb_analysis_plan();
-  p->serial = next_serial++;
-  p->device = d->device;
+  // (sizes whose products the tables and kernels form in 32-bit ints: far beyond any
+  // configuration, rejected before any arithmetic on them)
+  if (d->n_chan > (1 << 24) || d->os_nu > (1 << 16) || d->n_taps > ((int64_t)1 << 30))
+    return fail(PFB_ERR_UNSUPPORTED, "analysis parameters out of range (n_chan %d, os_nu %d, %lld taps)",
+                d->n_chan, d->os_nu, (long long)d->n_taps);
   p->variant = d->variant;
   p->N = d->n_chan;
   p->nu = d->os_nu;
@@ -433,53 +430,91 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
   p->n_taps = d->n_taps;
   p->P = (int)((d->n_taps + d->n_chan - 1) / d->n_chan);    // pad_filter.m:10
   p->n_pol = d->n_pol;
+  if (p->M <= 0) return fail(PFB_ERR_INVALID_ARG, "commutator step M = floor(N de/nu) is zero");
   p->sds = (int)std::ceil((double)(d->n_taps - 1) / 2.0 / (double)p->M);  // padded.m:89
-  if (p->M <= 0) {
-    delete p;
-    return fail(PFB_ERR_INVALID_ARG, "commutator step M = floor(N de/nu) is zero");
-  }
   p->C = p->N;
   if (p->variant == pfb::kLowCbf) {
     p->C = 216;
     p->lowcbf_pad = true;
     p->fused = true;
   } else if (!pfb::analysis_supported(p->N, p->P, p->variant, &p->fused)) {
-    delete p;
     return fail(PFB_ERR_UNSUPPORTED, "no analysis kernel for n_chan=%d", d->n_chan);
   }
-  if (hipSetDevice(p->device) != hipSuccess) {
-    delete p;
-    return fail(PFB_ERR_HIP, "hipSetDevice(%d) failed", d->device);
-  }
+  return PFB_OK;
+}
+
+// Host-side tables of an analysis plan
+struct AnaHost {
+  std::vector<float> taps, g;
+  std::vector<int> rev;
+};
+
+static void analysis_host_tables(const pfb_analysis_desc* d, const pfb_analysis_plan* p, AnaHost& h) {
   // zero rows up to the fused kernel's PMAX (32) so its tap loads are unconditional
-  std::vector<float> taps((size_t)std::max(p->P, 32) * p->N, 0.f);
-  for (int64_t i = 0; i < d->n_taps; ++i) taps[(size_t)i] = (float)d->taps[i];  // cast(filt, 'single')
-  hipError_t e = upload(p->taps, taps);
-  if (e == hipSuccess) e = upload(p->twN, twiddles(p->N, -1));
-  if (e == hipSuccess && analysis_emits_zblk(p) && p->N == 256) {
+  h.taps.assign((size_t)std::max(p->P, 32) * p->N, 0.f);
+  for (int64_t i = 0; i < d->n_taps; ++i) h.taps[(size_t)i] = (float)d->taps[i];  // cast(filt, 'single')
+  if (analysis_emits_zblk(p) && p->N == 256) {
     // g_s[m][c] = N^2 F[(m + 1) N + c - (s M mod N)], F = [N zeros, taps, zeros] — the
     // streaming kernel's folded taps (pfb_ana_stream.hpp), scaled by the power of two N^2
     // (exact), lags m < P + 1, zero-padded to 16 per (s, c)
     const int N = p->N, PE = p->P + 1;
     const float n2 = (float)N * (float)N;
-    std::vector<float> g((size_t)p->nu * N * 16, 0.f);
+    h.g.assign((size_t)p->nu * N * 16, 0.f);
     for (int sr = 0; sr < p->nu; ++sr) {
       const int as = (int)(((int64_t)sr * p->M) % N);
       for (int c = 0; c < N; ++c)
         for (int m = 0; m < PE; ++m) {
           const int j = (m + 1) * N + c - as;
-          const float f = (j >= N && j < (p->P + 1) * N) ? taps[(size_t)(j - N)] : 0.f;
-          g[((size_t)sr * N + c) * 16 + m] = n2 * f;
+          const float f = (j >= N && j < (p->P + 1) * N) ? h.taps[(size_t)(j - N)] : 0.f;
+          h.g[((size_t)sr * N + c) * 16 + m] = n2 * f;
         }
     }
-    e = upload(p->gtab, g);
   }
-  if (e == hipSuccess && !p->fused && p->variant == pfb::kPadded) {
-    std::vector<int> rev((size_t)p->N);
-    for (int i = 0; i < p->N; ++i) rev[(size_t)i] = (p->N - i) % p->N;
-    e = upload(p->zrev, rev);
+  if (!p->fused && p->variant == pfb::kPadded) {
+    h.rev.resize((size_t)p->N);
+    for (int i = 0; i < p->N; ++i) h.rev[(size_t)i] = (p->N - i) % p->N;
   }
+}
+
+static void analysis_release(pfb_analysis_plan* p) {
+  for (DevBuf* b : {&p->taps, &p->twN, &p->zrev, &p->gtab, &p->scratch, &p->carry, &p->work, &p->stage_in,
+                    &p->stage_out})
+    b->release();
+}
+
+pfb_status pfb_analysis_plan_validate(const pfb_analysis_desc* d) {
+  pfb_analysis_plan p;
+  const pfb_status st = analysis_validate(d, &p);
+  if (st != PFB_OK) return st;
+  AnaHost h;
+  analysis_host_tables(d, &p, h);
+  return PFB_OK;
+}
+
+pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_plan** out) {
+  if (!d || !out) return fail(PFB_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  pfb_analysis_plan tmp;
+  const pfb_status vst = analysis_validate(d, &tmp);
+  if (vst != PFB_OK) return vst;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(PFB_ERR_NO_DEVICE, "no HIP device available");
+  if (d->device < 0 || d->device >= ndev)
+    return fail(PFB_ERR_INVALID_ARG, "device %d out of range (%d devices)", d->device, ndev);
+  if (hipSetDevice(d->device) != hipSuccess) return fail(PFB_ERR_HIP, "hipSetDevice(%d) failed", d->device);
+  AnaHost h;
+  analysis_host_tables(d, &tmp, h);
+  static std::atomic<uint64_t> next_serial{1};
+  auto* p = new pfb_analysis_plan(tmp);
+  p->serial = next_serial++;
+  p->device = d->device;
+  hipError_t e = upload(p->taps, h.taps);
+  if (e == hipSuccess) e = upload(p->twN, twiddles(p->N, -1));
+  if (e == hipSuccess && !h.g.empty()) e = upload(p->gtab, h.g);
+  if (e == hipSuccess && !h.rev.empty()) e = upload(p->zrev, h.rev);
   if (e != hipSuccess) {
+    analysis_release(p);
     delete p;
     return fail(PFB_ERR_HIP, "analysis plan upload: %s", hipGetErrorString(e));
   }
@@ -490,15 +525,7 @@ pfb_status pfb_analysis_plan_create(const pfb_analysis_desc* d, pfb_analysis_pla
 pfb_status pfb_analysis_plan_destroy(pfb_analysis_plan* p) {
   if (!p) return PFB_OK;
   (void)hipSetDevice(p->device);
-  p->taps.release();
-  p->twN.release();
-  p->zrev.release();
-  p->gtab.release();
-  p->scratch.release();
-  p->carry.release();
-  p->work.release();
-  p->stage_in.release();
-  p->stage_out.release();
+  analysis_release(p);
   for (hipEvent_t e : p->events) (void)hipEventDestroy(e);
   if (p->aux) (void)hipStreamDestroy(p->aux);
   delete p;
@@ -988,20 +1015,26 @@ static pfb_status synthesis_run(pfb_synthesis_plan* p, const float2* in, int64_t
 
 extern "C" {
 
-pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_plan** out) {
-  if (!d || !out) return fail(PFB_ERR_INVALID_ARG, "null argument");
-  *out = nullptr;
+// Descriptor checks of pfb_synthesis_plan_create (no device needed)
+static pfb_status synthesis_validate(const pfb_synthesis_desc* d) {
+  if (!d) return fail(PFB_ERR_INVALID_ARG, "null argument");
   const int N = d->n_chan, nu = d->os_nu, de = d->os_de, Nf = d->input_fft_length,
             Ov = d->input_overlap;
   if (N <= 0 || nu <= 0 || de <= 0 || Nf <= 0 || Ov < 0 || d->n_pol <= 0)
     return fail(PFB_ERR_INVALID_ARG, "invalid synthesis parameters");
+  // (sizes whose products the tables and kernels form in 32-bit ints: far beyond any
+  // configuration, rejected before any arithmetic on them)
+  if (N > (1 << 24) || Nf > (1 << 24) || de > (1 << 16) || nu > (1 << 16))
+    return fail(PFB_ERR_UNSUPPORTED, "synthesis parameters out of range (n_chan %d, Nf %d, Ov %d, os %d/%d)",
+                N, Nf, Ov, nu, de);
   if (d->n_pol > 65535)  // polarisations map to grid.y of every launch
     return fail(PFB_ERR_INVALID_ARG, "n_pol = %d exceeds 65535 series per plan", d->n_pol);
   if (((int64_t)Nf * de) % nu != 0)
     return fail(PFB_ERR_INVALID_ARG, "input_fft_length*de/nu = %d*%d/%d is not integral", Nf, de, nu);
   if (((int64_t)Ov * de * N) % nu != 0)
     return fail(PFB_ERR_INVALID_ARG, "output_overlap = Ov*de/nu*n_chan is not integral");
-  if (Nf - 2 * Ov <= 0) return fail(PFB_ERR_INVALID_ARG, "input_keep = Nf - 2 Ov must be positive");
+  if ((int64_t)Nf - 2 * (int64_t)Ov <= 0)
+    return fail(PFB_ERR_INVALID_ARG, "input_keep = Nf - 2 Ov must be positive");
   const int W = (int)(((int64_t)Nf * de) / nu);
   if (W % 2 != 0) return fail(PFB_ERR_INVALID_ARG, "FN_width %d must be even", W);
   if (d->combine < 1 || N % d->combine != 0)
@@ -1031,43 +1064,50 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
     return fail(PFB_ERR_UNSUPPORTED,
                 "output_fft_length %lld or Nf x n_chan %lld exceeds a buffer descriptor "
                 "(%lld bytes)", (long long)W * N, (long long)Nf * N, (long long)pfb::kRsrcMaxBytes);
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
-    return fail(PFB_ERR_NO_DEVICE, "no HIP device available");
-  if (d->device < 0 || d->device >= ndev)
-    return fail(PFB_ERR_INVALID_ARG, "device %d out of range", d->device);
-  HIPCHK(hipSetDevice(d->device));
+  if (d->temporal_taper == PFB_WINDOW_CUSTOM && !d->temporal_coeffs)
+    return fail(PFB_ERR_INVALID_ARG, "CUSTOM temporal taper without coefficients");
+  if (d->temporal_taper < PFB_WINDOW_NONE || d->temporal_taper > PFB_WINDOW_CUSTOM)
+    return fail(PFB_ERR_INVALID_ARG, "unknown temporal taper %d", d->temporal_taper);
+  if (d->apply_deripple && (!d->taps || d->n_taps <= 0))
+    return fail(PFB_ERR_INVALID_ARG, "deripple requested without filter taps");
+  return PFB_OK;
+}
 
-  auto* p = new pfb_synthesis_plan();
-  p->device = d->device;
-  if (const char* v = pfb::knob("PFB_SYNTH_RANGES")) p->ranges = std::max(-1, std::atoi(v));
-  if (const char* v = pfb::knob("PFB_TIMING_MASK")) p->timing_mask = std::atoi(v);
-  if (const char* v = pfb::knob("PFB_SYNTH_NO_REUSE")) p->no_reuse = std::atoi(v) != 0;
-  if (const char* v = pfb::knob("PFB_SYNTH_XCD")) p->xcd = std::atoi(v) != 0;
-  if (const char* v = pfb::knob("PFB_RT_CHUNK_BLOCKS")) p->rt_chunk_blocks = std::max(1, std::atoi(v));
-  p->N = N;
-  p->nu = nu;
-  p->de = de;
-  p->Nf = Nf;
-  p->Ov = Ov;
-  p->spans = d->spans_nyquist ? 1 : 0;
-  p->combine = d->combine;
-  p->n_pol = d->n_pol;
-  p->W = W;
-  p->keep = Nf - 2 * Ov;
-  p->L = W * N;
-  p->Lov = (int)(((int64_t)Ov * de * N) / nu);
-  p->Lkeep = p->L - 2 * p->Lov;
+// Host-side tables of a synthesis plan (double maths, rounded once to float)
+struct SynthHost {
+  int N = 0, nu = 1, de = 1, Nf = 0, Ov = 0, W = 0, keep = 0, L = 0, Lov = 0, Lkeep = 0;
+  int t1_lo = 0, t1_hi = 0, spans = 1, combine = 1;
+  bool deripple = false, identity_perm = true, win_flat = false;
+  std::vector<float> window, cgain, taper, gj;
+  std::vector<int> perm;
+  std::vector<float2> tw4, tw4s;
+};
+
+static void synthesis_host_tables(const pfb_synthesis_desc* d, SynthHost& p) {
+  const int N = d->n_chan, nu = d->os_nu, de = d->os_de, Nf = d->input_fft_length, Ov = d->input_overlap;
+  const int W = (int)(((int64_t)Nf * de) / nu);
+  p.N = N;
+  p.nu = nu;
+  p.de = de;
+  p.Nf = Nf;
+  p.Ov = Ov;
+  p.spans = d->spans_nyquist ? 1 : 0;
+  p.combine = d->combine;
+  p.W = W;
+  p.keep = Nf - 2 * Ov;
+  p.L = W * N;
+  p.Lov = (int)(((int64_t)Ov * de * N) / nu);
+  p.Lkeep = p.L - 2 * p.Lov;
   // the kernels keep y[t0 + N t1] when L_ov <= t0 + N t1 < L - L_ov (sample-exact: L_ov =
   // Ov de/nu N need not be a multiple of N — normalize(os, Ov) = 40.5 for the reference's
   // 'sps' config); [t1_lo, t1_hi) bounds the t1 that hold any kept sample
-  p->t1_lo = p->Lov / N;
-  p->t1_hi = W - p->t1_lo;
-  p->deripple = d->apply_deripple != 0;
+  p.t1_lo = p.Lov / N;
+  p.t1_hi = W - p.t1_lo;
+  p.deripple = d->apply_deripple != 0;
 
   // temporal taper (PFBWindow.m) -> per-time window + per-channel gain (hann quirk)
-  std::vector<float> window((size_t)Nf, 1.f);
-  std::vector<float> cgain;
+  std::vector<float>& window = p.window;
+  window.assign((size_t)Nf, 1.f);
   switch (d->temporal_taper) {
     case PFB_WINDOW_NONE: break;
     case PFB_WINDOW_TUKEY: {
@@ -1087,50 +1127,41 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
       // PFBWindow.m:72-99: hann along dim 1 = channels; circshift when n_chan != Nf
       std::vector<double> h;
       hann_sym(N, h);
-      cgain.resize((size_t)N);
+      p.cgain.resize((size_t)N);
       for (int c = 0; c < N; ++c) {
         const int src = (N != Nf) ? ((c - N / 2) % N + N) % N : c;
-        cgain[(size_t)c] = (float)h[(size_t)src];
+        p.cgain[(size_t)c] = (float)h[(size_t)src];
       }
       break;
     }
     case PFB_WINDOW_CUSTOM:
-      if (!d->temporal_coeffs) {
-        delete p;
-        return fail(PFB_ERR_INVALID_ARG, "CUSTOM temporal taper without coefficients");
-      }
       for (int t = 0; t < Nf; ++t) window[(size_t)t] = (float)d->temporal_coeffs[t];
       break;
-    default:
-      delete p;
-      return fail(PFB_ERR_INVALID_ARG, "unknown temporal taper %d", d->temporal_taper);
+    default: break;  // rejected by synthesis_validate
   }
 
   // combine permutation (polyphase_synthesis.m:198-239): slot chan <- input jchan
-  std::vector<int> perm((size_t)N);
+  std::vector<int>& perm = p.perm;
+  perm.resize((size_t)N);
   for (int c = 0; c < N; ++c) perm[(size_t)c] = c;
-  if (p->combine > 1) {
-    const int fcc = N / p->combine, fco = N;
+  if (p.combine > 1) {
+    const int fcc = N / p.combine, fco = N;
     for (int chan = 0; chan < N; ++chan) {
       int fine = (chan + fcc / 2) % fco;
       int coarse = fine / fcc;
       fine -= coarse * fcc;
-      coarse = (coarse + p->combine / 2) % p->combine;
+      coarse = (coarse + p.combine / 2) % p.combine;
       fine = (fine + fcc / 2) % fcc;
       perm[(size_t)chan] = coarse * fcc + fine;
     }
   }
   for (int c = 0; c < N; ++c)
-    if (perm[(size_t)c] != c) p->identity_perm = false;
+    if (perm[(size_t)c] != c) p.identity_perm = false;
 
   // kept-bin tables (see oracle.synthesis_tables and DESIGN.md)
   const int W2 = W / 2, d2 = (Nf - W) / 2;
   std::vector<double> g(W2 + 1, 1.0);
-  if (p->deripple) {
-    if (!d->taps || d->n_taps <= 0) {
-      delete p;
-      return fail(PFB_ERR_INVALID_ARG, "deripple requested without filter taps");
-    }
+  if (p.deripple) {
     // H0 = freqz(h, 1, n), n = N*W/2; filter_response = 1/|H0(0..W/2)|  (:138-150)
     const int64_t nfz = (int64_t)N * W2;
     const int64_t two_n = 2 * nfz;
@@ -1149,7 +1180,7 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
   std::vector<double> gain((size_t)W);
   for (int jp = 0; jp < W; ++jp) {
     int j, e;
-    if (p->spans) {
+    if (p.spans) {
       j = (jp + W2) % W;
       e = (jp < W2) ? jp : jp - W;
     } else {
@@ -1161,53 +1192,113 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
     gain[(size_t)jp] = (j < W2) ? g[(size_t)(W2 - j)] : g[(size_t)(j - W2)];
   }
   // the rows the wave synthesis kernels treat as flat: [48, 208) at Nf 256, [128, 384) at 512
-  p->win_flat = (Nf == 256 || Nf == 512) &&
-                std::all_of(window.begin() + (Nf == 256 ? 48 : 128), window.begin() + (Nf == 256 ? 208 : 384),
-                            [](float w) { return w == 1.f; });
-  hipError_t e = upload(p->window, window);
+  p.win_flat = (Nf == 256 || Nf == 512) &&
+               std::all_of(window.begin() + (Nf == 256 ? 48 : 128), window.begin() + (Nf == 256 ? 208 : 384),
+                           [](float w) { return w == 1.f; });
   // four-step twiddle x deripple gain, laid out [j'][t0] (coalesced in the block kernel)
-  std::vector<float2> tw4((size_t)N * W), tw4s((size_t)N * W);
-  const double oscale = (double)p->de / (double)p->nu / (double)p->L;
+  p.tw4.resize((size_t)N * W);
+  p.tw4s.resize((size_t)N * W);
+  const double oscale = (double)p.de / (double)p.nu / (double)p.L;
   for (int t0 = 0; t0 < N; ++t0) {
     for (int jp = 0; jp < W; ++jp) {
-      int64_t m = ((int64_t)t0 * expo[(size_t)jp]) % p->L;
-      if (m < 0) m += p->L;
-      if (2 * m > p->L) m -= p->L;
-      const double ang = 2.0 * M_PI * (double)m / (double)p->L;
+      int64_t m = ((int64_t)t0 * expo[(size_t)jp]) % p.L;
+      if (m < 0) m += p.L;
+      if (2 * m > p.L) m -= p.L;
+      const double ang = 2.0 * M_PI * (double)m / (double)p.L;
       const double gj = gain[(size_t)jp];
-      tw4[(size_t)jp * N + t0] = make_float2((float)(gj * std::cos(ang)), (float)(gj * std::sin(ang)));
-      tw4s[(size_t)jp * N + t0] =
+      p.tw4[(size_t)jp * N + t0] = make_float2((float)(gj * std::cos(ang)), (float)(gj * std::sin(ang)));
+      p.tw4s[(size_t)jp * N + t0] =
           make_float2((float)(oscale * gj * std::cos(ang)), (float)(oscale * gj * std::sin(ang)));
     }
   }
-  if (e == hipSuccess) e = upload(p->tw4, tw4);
-  if (e == hipSuccess) e = upload(p->tw4s, tw4s);
-  if (e == hipSuccess) e = upload(p->perm, perm);
-  if (e == hipSuccess && !cgain.empty()) {
-    e = upload(p->cgain, cgain);
-    p->has_cgain = true;
-  }
-  if (e == hipSuccess) e = upload(p->twN, twiddles(N, -1));
-  if (e == hipSuccess) e = upload(p->twNf, twiddles(Nf, -1));
-  if (e == hipSuccess) e = upload(p->twW, twiddles(W, -1));
-  if (e == hipSuccess && d->spectral_taper != PFB_WINDOW_NONE) {
-    p->has_spectral = true;
-    std::vector<float> taper((size_t)p->L);
+  if (d->spectral_taper != PFB_WINDOW_NONE) {
+    p.taper.resize((size_t)p.L);
     if (d->spectral_taper == PFB_WINDOW_HANN) {
       // hann(L) circularly shifted by L/2 (PFBWindow.m:83-95: ndat = L != Nf)
       std::vector<double> h;
-      hann_sym(p->L, h);
-      for (int i = 0; i < p->L; ++i) taper[(size_t)i] = (float)h[(size_t)((i - p->L / 2 + p->L) % p->L)];
+      hann_sym(p.L, h);
+      for (int i = 0; i < p.L; ++i) p.taper[(size_t)i] = (float)h[(size_t)((i - p.L / 2 + p.L) % p.L)];
     } else {
-      for (int i = 0; i < p->L; ++i) taper[(size_t)i] = (float)d->spectral_coeffs[i];
+      for (int i = 0; i < p.L; ++i) p.taper[(size_t)i] = (float)d->spectral_coeffs[i];
     }
     // deripple gains in Matlab's FN row order j (polyphase_synthesis.m:244-250)
-    std::vector<float> gj((size_t)W);
-    for (int j = 0; j < W; ++j) gj[(size_t)j] = (float)((j < W2) ? g[(size_t)(W2 - j)] : g[(size_t)(j - W2)]);
-    e = upload(p->taper, taper);
-    if (e == hipSuccess) e = upload(p->gainj, gj);
+    p.gj.resize((size_t)W);
+    for (int j = 0; j < W; ++j) p.gj[(size_t)j] = (float)((j < W2) ? g[(size_t)(W2 - j)] : g[(size_t)(j - W2)]);
+  }
+}
+
+static void synthesis_release(pfb_synthesis_plan* p) {
+  for (DevBuf* b : {&p->window, &p->tw4, &p->tw4s, &p->twN, &p->twNf, &p->twW, &p->perm, &p->cgain,
+                    &p->taper, &p->gainj, &p->sbuf0, &p->sbuf1, &p->Z, &p->carry, &p->work,
+                    &p->stage_in, &p->stage_out})
+    b->release();
+}
+
+pfb_status pfb_synthesis_plan_validate(const pfb_synthesis_desc* d) {
+  const pfb_status st = synthesis_validate(d);
+  if (st != PFB_OK) return st;
+  SynthHost h;
+  synthesis_host_tables(d, h);
+  return PFB_OK;
+}
+
+pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_plan** out) {
+  if (!d || !out) return fail(PFB_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  const pfb_status vst = synthesis_validate(d);
+  if (vst != PFB_OK) return vst;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(PFB_ERR_NO_DEVICE, "no HIP device available");
+  if (d->device < 0 || d->device >= ndev)
+    return fail(PFB_ERR_INVALID_ARG, "device %d out of range", d->device);
+  HIPCHK(hipSetDevice(d->device));
+
+  SynthHost h;
+  synthesis_host_tables(d, h);
+  auto* p = new pfb_synthesis_plan();
+  p->device = d->device;
+  if (const char* v = pfb::knob("PFB_SYNTH_RANGES")) p->ranges = std::max(-1, std::atoi(v));
+  if (const char* v = pfb::knob("PFB_TIMING_MASK")) p->timing_mask = std::atoi(v);
+  if (const char* v = pfb::knob("PFB_SYNTH_NO_REUSE")) p->no_reuse = std::atoi(v) != 0;
+  if (const char* v = pfb::knob("PFB_SYNTH_XCD")) p->xcd = std::atoi(v) != 0;
+  if (const char* v = pfb::knob("PFB_RT_CHUNK_BLOCKS")) p->rt_chunk_blocks = std::max(1, std::atoi(v));
+  p->N = h.N;
+  p->nu = h.nu;
+  p->de = h.de;
+  p->Nf = h.Nf;
+  p->Ov = h.Ov;
+  p->spans = h.spans;
+  p->combine = h.combine;
+  p->n_pol = d->n_pol;
+  p->W = h.W;
+  p->keep = h.keep;
+  p->L = h.L;
+  p->Lov = h.Lov;
+  p->Lkeep = h.Lkeep;
+  p->t1_lo = h.t1_lo;
+  p->t1_hi = h.t1_hi;
+  p->deripple = h.deripple;
+  p->identity_perm = h.identity_perm;
+  p->win_flat = h.win_flat;
+  hipError_t e = upload(p->window, h.window);
+  if (e == hipSuccess) e = upload(p->tw4, h.tw4);
+  if (e == hipSuccess) e = upload(p->tw4s, h.tw4s);
+  if (e == hipSuccess) e = upload(p->perm, h.perm);
+  if (e == hipSuccess && !h.cgain.empty()) {
+    e = upload(p->cgain, h.cgain);
+    p->has_cgain = true;
+  }
+  if (e == hipSuccess) e = upload(p->twN, twiddles(h.N, -1));
+  if (e == hipSuccess) e = upload(p->twNf, twiddles(h.Nf, -1));
+  if (e == hipSuccess) e = upload(p->twW, twiddles(h.W, -1));
+  if (e == hipSuccess && d->spectral_taper != PFB_WINDOW_NONE) {
+    p->has_spectral = true;
+    e = upload(p->taper, h.taper);
+    if (e == hipSuccess) e = upload(p->gainj, h.gj);
   }
   if (e != hipSuccess) {
+    synthesis_release(p);
     delete p;
     return fail(PFB_ERR_HIP, "synthesis plan upload: %s", hipGetErrorString(e));
   }
@@ -1218,10 +1309,7 @@ pfb_status pfb_synthesis_plan_create(const pfb_synthesis_desc* d, pfb_synthesis_
 pfb_status pfb_synthesis_plan_destroy(pfb_synthesis_plan* p) {
   if (!p) return PFB_OK;
   (void)hipSetDevice(p->device);
-  for (DevBuf* b : {&p->window, &p->tw4, &p->tw4s, &p->twN, &p->twNf, &p->twW, &p->perm, &p->cgain,
-                    &p->taper, &p->gainj, &p->sbuf0, &p->sbuf1, &p->Z, &p->carry, &p->work,
-                    &p->stage_in, &p->stage_out})
-    b->release();
+  synthesis_release(p);
   delete p;
   return PFB_OK;
 }

@@ -76,6 +76,7 @@ class SynthesisDesc(Structure):
 SYMBOLS = [
     ("pfb_analysis_plan_create", c_int32, [POINTER(AnalysisDesc), POINTER(c_void_p)]),
     ("pfb_analysis_plan_destroy", c_int32, [c_void_p]),
+    ("pfb_analysis_plan_validate", c_int32, [POINTER(AnalysisDesc)]),
     ("pfb_analysis_output_length", c_int64, [c_void_p, c_int64]),
     ("pfb_analysis_output_channels", c_int32, [c_void_p]),
     ("pfb_analysis_execute", c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64,
@@ -90,6 +91,7 @@ SYMBOLS = [
                                                  c_int32, c_int64, POINTER(c_int64), c_void_p]),
     ("pfb_synthesis_plan_create", c_int32, [POINTER(SynthesisDesc), POINTER(c_void_p)]),
     ("pfb_synthesis_plan_destroy", c_int32, [c_void_p]),
+    ("pfb_synthesis_plan_validate", c_int32, [POINTER(SynthesisDesc)]),
     ("pfb_synthesis_output_length", c_int64, [c_void_p, c_int64]),
     ("pfb_synthesis_execute", c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
                                         c_int64, c_int64, POINTER(c_int64), c_int32, c_void_p]),
