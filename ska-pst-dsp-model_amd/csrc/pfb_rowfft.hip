@@ -8,6 +8,143 @@
 
 namespace pfb {
 
+// ----------------------------------------------------------------- 4096-point row FFT
+// The SKA-Mid row FFT (the analysis FFT of polyphase_analysis_padded.m:147 for C3, and the
+// synthesis stage 1 of 4096-channel rows) as three explicit radix-16 Stockham passes per
+// row, persistent over a contiguous row range (XCD-aware), next row prefetched into
+// registers.  Round 5: the twiddles come from per-pass power tables instead of strided
+// reads of one 4096-entry table — pass 3 read table entries r k at lane stride r = 2, 4, 8
+// (2-, 4- and 8-way LDS bank conflicts, 24 % of the kernel's LDS cycles) — each lane now
+// reads w^{2^p}(k) from T3[p][k], contiguous in k (conflict-free).  The entries are the
+// same table values (e^{-2 pi i m / 4096}, rounded once from double on the host) and the
+// other powers are the same products, so the output is bit-identical to the generic
+// passes.  The tables take 8.7 KB instead of 32 KB of LDS: 3 workgroups per CU.
+constexpr int kR4kTw2 = 4 * 16;    // T2[p][k] = tw[(2^p 16 k) mod N], k < 16
+constexpr int kR4kTw3 = 4 * 256;   // T3[p][k] = tw[2^p k], k < 256
+constexpr size_t kR4kLds = ((size_t)lds_row(4096) + kR4kTw2 + kR4kTw3) * sizeof(float2);
+
+template <int DIR>
+__device__ __forceinline__ void r4k_twiddles(const float2* t, int k, int stride, float2 (&w)[16]) {
+  static_for<0, 4>([&](auto pv) {
+    constexpr int p = decltype(pv)::value;
+    float2 v = t[p * stride + k];
+    if constexpr (DIR > 0) v.y = -v.y;
+    w[1 << p] = v;
+  });
+  static_for<1, 16>([&](auto rv) {
+    constexpr int r = decltype(rv)::value;
+    constexpr int h = high_bit(r);
+    if constexpr (h != r) w[r] = cmul(w[h], w[r - h]);
+  });
+}
+
+// (buffer loads / stores: one descriptor per row, the lane's byte offset tid * 8 and the
+// register's r * 2048 as a scalar offset — no 64-bit address per register: <= 168 VGPRs,
+// 3 workgroups per CU)
+template <int DIR, bool PERM, bool GAIN>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void row_fft4096_kernel(RowFftArgs a) {
+  constexpr int N = 4096;
+  extern __shared__ __attribute__((aligned(16))) float2 smem[];
+  const int pol = blockIdx.y;
+  const int wg = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t q0 = a.n_rows * wg / gridDim.x, q1 = a.n_rows * (wg + 1) / gridDim.x;
+  if (q0 >= q1) return;  // uniform per workgroup
+  const int tid = threadIdx.x;
+  float2* row = smem;                        // lpad layout, lds_row(N) slots
+  float2* t2 = smem + lds_row(N);            // [p][16]
+  float2* t3 = t2 + kR4kTw2;                 // [p][256]
+  for (int e = tid; e < kR4kTw3; e += NT) {
+    const int pp = e >> 8, k = e & 255;
+    t3[e] = a.tw[(k << pp) & (N - 1)];
+    if (e < kR4kTw2) t2[e] = a.tw[((e & 15) << ((e >> 4) + 4)) & (N - 1)];
+  }
+  const float2* in = a.in + pol * a.in_pol_stride;
+  float2* out = a.out + pol * a.out_pol_stride;
+  [[maybe_unused]] uint32_t col[PERM ? 16 : 1];
+  [[maybe_unused]] float g[GAIN ? 16 : 1];
+  if constexpr (PERM || GAIN) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = tid + r * 256;
+      const int c = PERM ? a.perm[i] : i;
+      if constexpr (PERM) col[PERM ? r : 0] = (uint32_t)c * 8u;
+      if constexpr (GAIN) g[GAIN ? r : 0] = a.cgain[c];
+    }
+  }
+  const uint32_t lane_off = (uint32_t)tid * 8u;
+  float2 pf[16];
+  auto load_row = [&](int64_t rr) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + rr * N, (uint32_t)(N * 8));
+    static_for<0, 16>([&](auto rv) {
+      constexpr int r = decltype(rv)::value;
+      const v2u x = PERM ? __builtin_amdgcn_raw_buffer_load_b64(rs, col[PERM ? r : 0], 0, kNtlRow ? 2 : 0)
+                         : __builtin_amdgcn_raw_buffer_load_b64(rs, lane_off, r * 2048, kNtlRow ? 2 : 0);
+      pf[r] = __builtin_bit_cast(float2, x);
+    });
+  };
+  load_row(q0);
+  const int k2 = tid & 15;
+  const int st2 = (tid >> 4) * 256 + k2;     // pass-2 output base (j / 16) 256 + k
+#pragma unroll 1
+  for (int64_t rw = q0; rw < q1; ++rw) {
+    float2 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = GAIN ? cscale(pf[r], g[GAIN ? r : 0]) : pf[r];
+    load_row(min(rw + 1, q1 - 1));  // unconditional: past the end re-reads the last row
+    __syncthreads();  // tables staged / the previous row's pass 3 is done with the LDS row
+    // pass 1 (NS 1): no twiddles, outputs tid 16 + r
+    sdft<16, DIR>(v);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) row[lpad(tid * 16 + r)] = v[r];
+    __syncthreads();
+    // pass 2 (NS 16): k = tid mod 16, twiddles w^r, r = 1..15, of m = 16 k
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = row[lpad(tid + 256 * r)];
+    {
+      float2 w[16];
+      r4k_twiddles<DIR>(t2, k2, 16, w);
+      static_for<1, 16>([&](auto r) { v[r] = cmul(v[r], w[r]); });
+    }
+    sdft<16, DIR>(v);
+    __syncthreads();  // every pass-2 load done before the in-place stores
+#pragma unroll
+    for (int r = 0; r < 16; ++r) row[lpad(st2 + 16 * r)] = v[r];
+    __syncthreads();
+    // pass 3 (NS 256): k = tid, twiddles of m = k; outputs tid + 256 r -> HBM
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = row[lpad(tid + 256 * r)];
+    {
+      float2 w[16];
+      r4k_twiddles<DIR>(t3, tid, 256, w);
+      static_for<1, 16>([&](auto r) { v[r] = cmul(v[r], w[r]); });
+    }
+    sdft<16, DIR>(v);
+    // output row: row_base + rw, circularly shifted by -sds mod n_total (the padded
+    // variant's time shift, RowStore's rule)
+    int64_t t = a.row_base + rw;
+    if (a.remap) {
+      t -= a.sds;
+      while (t < 0) t += a.n_total;
+    }
+    const __amdgpu_buffer_rsrc_t os = make_rsrc(out + t * N, (uint32_t)(N * 8));
+    static_for<0, 16>([&](auto rv) {
+      constexpr int r = decltype(rv)::value;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v[r], a.scale)), os, lane_off,
+                                            r * 2048, kNtRow ? 2 : 0);
+    });
+  }
+}
+
+template <int DIR, bool PERM, bool GAIN>
+static hipError_t launch_row_fft4096(const RowFftArgs& r, int n_pol, hipStream_t s, int per_cu) {
+  auto kern = row_fft4096_kernel<DIR, PERM, GAIN>;
+  hipError_t e = set_lds(kern, kR4kLds);
+  if (e != hipSuccess) return e;
+  const int64_t wgs = (int64_t)cu_count() * per_cu;
+  dim3 grid((unsigned)std::max<int64_t>(1, wgs / n_pol), (unsigned)n_pol);
+  return launch_kernel(kern, grid, dim3(NT), kR4kLds, s, r);
+}
+
 template <int N, int DIR, bool PERM, bool GAIN>
 static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s) {
   constexpr int ROWS = RowShape<N>::ROWS;
@@ -24,6 +161,14 @@ static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s
     // a concurrent synthesis — experiments A/B)
     static const int env_wgs = knob("PFB_ROWFFT_WGS") ? std::atoi(knob("PFB_ROWFFT_WGS")) : 0;
     if (env_wgs > 0) wgs = env_wgs;
+    // the explicit-pass kernel with per-pass twiddle tables (PFB_ROWFFT_4K=0: the generic
+    // persistent kernel; PFB_ROWFFT_WPC: its workgroups per CU, default the 3 LDS allows —
+    // experiments A/B)
+    static const bool k4 = !(knob("PFB_ROWFFT_4K") && std::atoi(knob("PFB_ROWFFT_4K")) == 0);
+    static const int wpc = knob("PFB_ROWFFT_WPC") ? std::atoi(knob("PFB_ROWFFT_WPC")) : 0;
+    const int per_cu4 = wpc > 0 ? wpc : (int)std::max<size_t>(1, std::min<size_t>(3, (160 * 1024) / kR4kLds));
+    if (!off && k4 && env_wgs <= 0 && r.n_rows >= 4 * (int64_t)cu_count() * per_cu4)
+      return launch_row_fft4096<DIR, PERM, GAIN>(r, n_pol, s, per_cu4);
     if (!off && r.n_rows >= 4 * wgs) {
       // (PFB_ROWFFT_PF=2: two rows prefetched ahead, experiments A/B)
       auto kern = row_fft_persist_kernel<N, DIR, PERM, GAIN, 1>;
