@@ -554,11 +554,10 @@ static hipError_t launch_fir_lds_t(const AnalysisArgs& a, hipStream_t s) {
       return hipGetLastError();
     }
   }
+  // (launch_kernel: timed by the profiler's armed events like every other single launch)
   if (a.variant == kBunton)
-    hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kBunton>), grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);
-  else
-    hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kPadded>), grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);
-  return hipGetLastError();
+    return launch_kernel(fir_lds_kernel<PW, DE, NU, kBunton>, grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);
+  return launch_kernel(fir_lds_kernel<PW, DE, NU, kPadded>, grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);
 }
 
 template <int PW, int DE>
@@ -592,9 +591,9 @@ static hipError_t launch_fir_window_t(const AnalysisArgs& a, hipStream_t s) {
     // (wide DE: the U DE loads in flight would not fit the register budget)
     constexpr int U = DE * decltype(u)::value <= 21 ? decltype(u)::value : 1;
     if (a.variant == kBunton)
-      hipLaunchKernelGGL((fir_window_kernel<PW, DE, kBunton, U>), grid, dim3(NT), 0, s, a, ranges, slice_map);
+      (void)launch_kernel(fir_window_kernel<PW, DE, kBunton, U>, grid, dim3(NT), 0, s, a, ranges, slice_map);
     else
-      hipLaunchKernelGGL((fir_window_kernel<PW, DE, kPadded, U>), grid, dim3(NT), 0, s, a, ranges, slice_map);
+      (void)launch_kernel(fir_window_kernel<PW, DE, kPadded, U>, grid, dim3(NT), 0, s, a, ranges, slice_map);
   };
   if (rows == 1) go(std::integral_constant<int, 1>{});
   else if (rows == 2) go(std::integral_constant<int, 2>{});

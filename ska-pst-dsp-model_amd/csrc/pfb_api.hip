@@ -913,13 +913,15 @@ static pfb_status synthesis_chunk(pfb_synthesis_plan* p, const float2* in, int64
   c.perm = p->identity_perm ? nullptr : p->perm.as<int>();
   c.cgain = p->has_cgain ? p->cgain.as<float>() : nullptr;
   c.twN = p->twN.as<float2>();
+  // the Nf = 256 shapes: Z in the 2-row run layout the wave kernel reads (256-B runs per
+  // load instruction, as the fused round trip's analysis writes it); every other shape
+  // [row][t0] for the block kernel
+  const int zb = pfb::synth_wave_supported(synth_args(p, Z, rows * p->N, b0, nb, out, out_ps, out_limit, 2)) ? 2 : 0;
+  c.zblk = zb ? zb : 1;
   {
     ProfScope ps(1, (double)p->n_pol * rows * p->N * 16.0, s);
     HIPCHK(pfb::launch_chan_ifft(c, s));
   }
-  // Z is [row][t0] (run length 1): the Nf = 256 shapes take the wave kernel on it, as the
-  // fused round trip does on its run layout (the block kernel: every other shape)
-  const int zb = pfb::synth_wave_supported(synth_args(p, Z, rows * p->N, b0, nb, out, out_ps, out_limit, 1)) ? 1 : 0;
   return synthesis_blocks(p, Z, rows * p->N, b0, nb, out, out_ps, out_limit, s, zb);
 }
 

@@ -105,6 +105,7 @@ struct ChanIfftArgs {
   const int* perm;         // slot -> input channel (null = identity)
   const float* cgain;      // per-slot gain (null = 1)
   const float2* twN;
+  int zblk = 1;            // Z rows in runs of zblk (1, 2, 4) per t0 (SynthBlockArgs::zblk)
 };
 
 // Synthesis stage 2: per block and group of t0, Nf-point FFT over time, kept-bin

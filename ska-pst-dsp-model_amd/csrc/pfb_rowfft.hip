@@ -167,7 +167,7 @@ static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s
     static const bool k4 = !(knob("PFB_ROWFFT_4K") && std::atoi(knob("PFB_ROWFFT_4K")) == 0);
     static const int wpc = knob("PFB_ROWFFT_WPC") ? std::atoi(knob("PFB_ROWFFT_WPC")) : 0;
     const int per_cu4 = wpc > 0 ? wpc : (int)std::max<size_t>(1, std::min<size_t>(3, (160 * 1024) / kR4kLds));
-    if (!off && k4 && env_wgs <= 0 && r.n_rows >= 4 * (int64_t)cu_count() * per_cu4)
+    if (!off && k4 && env_wgs <= 0 && r.zs == 0 && r.n_rows >= 4 * (int64_t)cu_count() * per_cu4)
       return launch_row_fft4096<DIR, PERM, GAIN>(r, n_pol, s, per_cu4);
     if (!off && r.n_rows >= 4 * wgs) {
       // (PFB_ROWFFT_PF=2: two rows prefetched ahead, experiments A/B)
@@ -249,7 +249,8 @@ bool chan_ifft_supported(int N) { return pow2_supported(N) || mixed_chan_support
 hipError_t launch_chan_ifft(const ChanIfftArgs& c, hipStream_t s) {
   if (c.n_rows <= 0) return hipSuccess;
   RowFftArgs r{c.in, c.in_pol_stride, c.out, c.out_pol_stride, c.n_rows, c.perm, c.cgain, c.twN,
-               1.0f, 0, 0, 0, c.n_rows};
+               1.0f, 0, 0, 0, c.n_rows, c.zblk == 4 ? 2 : c.zblk == 2 ? 1 : 0};
+  if (c.zblk != 1 && c.zblk != 2 && c.zblk != 4) return hipErrorInvalidValue;
   return dispatch_row_fft<+1>(c.N, r, c.n_pol, s);
 }
 

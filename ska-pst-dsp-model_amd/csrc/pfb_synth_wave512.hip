@@ -80,14 +80,18 @@ __device__ __forceinline__ void lds_pair2(const char* p, float2& a, float2& b) {
   b = make_float2(q.z, q.w);
 }
 
-// the value of the other lane of the pair (lane ^ 1)
-__device__ __forceinline__ float pair_swap(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1 /* quad_perm 1,0,3,2 */, 0xF, 0xF,
-                                                 false));
+// a + sg * (the value of the other lane of the pair, lane ^ 1): ONE v_fmac_f32 with the DPP
+// swizzle quad_perm:[1,0,3,2] on its first source (the compiler does not fuse a separate
+// v_mov_b32_dpp into the fma: 30 VALU instructions a block saved; its hazard recognizer
+// places the wait states the DPP read needs)
+__device__ __forceinline__ float pair_fma(float a, float sg) {
+  float r;
+  asm("v_fmac_f32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(a), "v"(sg), "0"(a));
+  return r;
 }
 // self + sg * partner
 __device__ __forceinline__ float2 pair_bfly(float2 a, float sg) {
-  return make_float2(fmaf(pair_swap(a.x), sg, a.x), fmaf(pair_swap(a.y), sg, a.y));
+  return make_float2(pair_fma(a.x, sg), pair_fma(a.y, sg));
 }
 
 // v[i] *= row[i], i < 2 NP (one ds_read_b128 per pair, multiplied as it arrives)
@@ -312,9 +316,10 @@ void synth_wave512_kernel(SynthBlockArgs a) {
       // lanes t1a >= 28 hold no output: their offsets leave the descriptor's range
       int base = (t1a < 28) ? (t1a * N + t0g + col2) * 8 : (int)0x80000000;
       asm volatile("" : "+v"(base));
+      // (the row offsets t 28 N 8 are uniform: scalar offsets, one lane offset register)
       static_for<0, 8>([&](auto t) {
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y[t]), o,
-                                              (uint32_t)(base + t * 28 * N * 8), 0, kNtW5 ? 2 : 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y[t]), o, (uint32_t)base,
+                                              t * 28 * N * 8, kNtW5 ? 2 : 0);
       });
     }
   }
