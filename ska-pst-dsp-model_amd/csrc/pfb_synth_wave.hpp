@@ -390,10 +390,11 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       int base = (t1a < RW) ? (t1a * N - a.Lov + t0g + col2) * 8 : (int)0x80000000;
       // (FIR variant: recomputed every block — 16 hoisted store offsets would spill)
       if constexpr (FIRV::kOn) asm volatile("" : "+v"(base));
-      // (the row offsets t RW N 8 are uniform: scalar offsets, one lane offset register)
+      // (the whole offset in the lane register: the buffer range check covers the lane
+      // offset, not a scalar offset, and discards the negative t1 < t1_lo offsets)
       static_for<0, 16>([&](auto t) {
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v[t]), o, (uint32_t)base,
-                                              t * RW * N * 8, kAuxOut);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v[t]), o,
+                                              (uint32_t)(base + t * RW * N * 8), 0, kAuxOut);
       });
     }
     if constexpr (PRIO & 2) __builtin_amdgcn_s_setprio(0);

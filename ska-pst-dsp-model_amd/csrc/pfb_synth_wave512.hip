@@ -316,10 +316,11 @@ void synth_wave512_kernel(SynthBlockArgs a) {
       // lanes t1a >= 28 hold no output: their offsets leave the descriptor's range
       int base = (t1a < 28) ? (t1a * N + t0g + col2) * 8 : (int)0x80000000;
       asm volatile("" : "+v"(base));
-      // (the row offsets t 28 N 8 are uniform: scalar offsets, one lane offset register)
+      // (the whole offset in the lane register: the buffer range check covers the lane
+      // offset, not a scalar offset — a ragged last block must drop its tail stores)
       static_for<0, 8>([&](auto t) {
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y[t]), o, (uint32_t)base,
-                                              t * 28 * N * 8, kNtW5 ? 2 : 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y[t]), o,
+                                              (uint32_t)(base + t * 28 * N * 8), 0, kNtW5 ? 2 : 0);
       });
     }
   }
