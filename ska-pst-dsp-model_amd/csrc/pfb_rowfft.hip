@@ -136,11 +136,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void ro
 }
 
 template <int DIR, bool PERM, bool GAIN>
-static hipError_t launch_row_fft4096(const RowFftArgs& r, int n_pol, hipStream_t s, int per_cu) {
+static hipError_t launch_row_fft4096(const RowFftArgs& r, int n_pol, hipStream_t s, int per_cu, int wgs_override) {
   auto kern = row_fft4096_kernel<DIR, PERM, GAIN>;
   hipError_t e = set_lds(kern, kR4kLds);
   if (e != hipSuccess) return e;
-  const int64_t wgs = (int64_t)cu_count() * per_cu;
+  const int64_t wgs = wgs_override > 0 ? wgs_override : (int64_t)cu_count() * per_cu;
   dim3 grid((unsigned)std::max<int64_t>(1, wgs / n_pol), (unsigned)n_pol);
   return launch_kernel(kern, grid, dim3(NT), kR4kLds, s, r);
 }
@@ -167,8 +167,8 @@ static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s
     static const bool k4 = !(knob("PFB_ROWFFT_4K") && std::atoi(knob("PFB_ROWFFT_4K")) == 0);
     static const int wpc = knob("PFB_ROWFFT_WPC") ? std::atoi(knob("PFB_ROWFFT_WPC")) : 0;
     const int per_cu4 = wpc > 0 ? wpc : (int)std::max<size_t>(1, std::min<size_t>(3, (160 * 1024) / kR4kLds));
-    if (!off && k4 && env_wgs <= 0 && r.zs == 0 && r.n_rows >= 4 * (int64_t)cu_count() * per_cu4)
-      return launch_row_fft4096<DIR, PERM, GAIN>(r, n_pol, s, per_cu4);
+    if (!off && k4 && r.zs == 0 && r.n_rows >= 4 * (int64_t)cu_count() * per_cu4)
+      return launch_row_fft4096<DIR, PERM, GAIN>(r, n_pol, s, per_cu4, env_wgs);
     if (!off && r.n_rows >= 4 * wgs) {
       // (PFB_ROWFFT_PF=2: two rows prefetched ahead, experiments A/B)
       auto kern = row_fft_persist_kernel<N, DIR, PERM, GAIN, 1>;
