@@ -1,0 +1,50 @@
+"""A few steps of one workload for rocprofv3 --pmc passes (scripts/gpu_pmc_r05.sh):
+c2 = the fused C2 round trip (bench.py's step), c2syn = the standalone C2 synthesis
+(SynthesisPlan.execute of an HBM-resident channelised product), c3 = the SKA-Mid round trip.
+Every kernel name then maps to one workload in profiles/pmc_traffic.json."""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "ska-pst-dsp-model_amd"), REPO]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=("c2", "c2syn", "c3"), required=True)
+    ap.add_argument("--steps", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+    import ska_pst_dsp_model_amd as pfb
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(100)
+    if args.workload == "c3":
+        taps = pfb.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
+        N, nf, ov, var, n = 4096, 512, 128, "polyphase_analysis_padded", 1 << 26
+    else:
+        taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
+        N, nf, ov, var, n = 256, 256, 48, "polyphase_analysis", 1 << 24
+    x = (torch.complex(torch.randn((1, n), device=dev, generator=g),
+                       torch.randn((1, n), device=dev, generator=g)) / np.sqrt(2)).to(torch.complex64)
+    ana = pfb.AnalysisPlan(taps, N, "8/7", var, 1, 0)
+    win = pfb.PFBWindow().lookup["tukey"](nf, ov)
+    syn = pfb.SynthesisPlan(N, "8/7", nf, ov, True, 1, True, taps, win, None, 1, 0)
+    if args.workload == "c2syn":
+        chan = ana.execute(x).contiguous()
+        torch.cuda.synchronize()
+        for _ in range(args.steps):
+            syn.execute(chan, layout="ptc")
+    else:
+        K = ana.output_length(n)
+        chan = torch.empty((1, K, N), dtype=torch.complex64, device=dev)
+        out = torch.empty((1, syn.output_length(K)), dtype=torch.complex64, device=dev)
+        for _ in range(args.steps):
+            pfb.roundtrip(ana, syn, x, chan=chan, out=out)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()
