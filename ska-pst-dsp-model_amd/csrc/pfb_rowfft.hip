@@ -19,9 +19,17 @@ namespace pfb {
 // same table values (e^{-2 pi i m / 4096}, rounded once from double on the host) and the
 // other powers are the same products, so the output is bit-identical to the generic
 // passes.  The tables take 8.7 KB instead of 32 KB of LDS: 3 workgroups per CU.
+// The row takes two layouts instead of the 1-in-16 pad (whose pass-2 / pass-3 loads wrapped
+// one lane of every 32-lane ds_read_b64 group onto bank 0: 2-way, 22 % of the LDS cycles,
+// r05_v4 PMC): pass 1 -> pass 2, element 16 j + r at slot 258 r + j (rows of 258 slots: the
+// 16-lane store groups and the 32-lane load groups, 258 (tid mod 16) + tid / 16, on distinct
+// banks); pass 2 -> pass 3 unpadded (element e at slot e).  Every access is one lane base
+// plus an immediate offset.
+constexpr int kR4kA = 258;         // layout-A row of 16 j + r: slot kR4kA r + j (258 = 2 mod 32)
+constexpr int kR4kRow = 15 * kR4kA + 256 + 2;  // slots of the row buffer (layout A; B needs 4096)
 constexpr int kR4kTw2 = 4 * 16;    // T2[p][k] = tw[(2^p 16 k) mod N], k < 16
 constexpr int kR4kTw3 = 4 * 256;   // T3[p][k] = tw[2^p k], k < 256
-constexpr size_t kR4kLds = ((size_t)lds_row(4096) + kR4kTw2 + kR4kTw3) * sizeof(float2);
+constexpr size_t kR4kLds = ((size_t)kR4kRow + kR4kTw2 + kR4kTw3) * sizeof(float2);
 
 template <int DIR>
 __device__ __forceinline__ void r4k_twiddles(const float2* t, int k, int stride, float2 (&w)[16]) {
@@ -50,8 +58,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void ro
   const int64_t q0 = a.n_rows * wg / gridDim.x, q1 = a.n_rows * (wg + 1) / gridDim.x;
   if (q0 >= q1) return;  // uniform per workgroup
   const int tid = threadIdx.x;
-  float2* row = smem;                        // lpad layout, lds_row(N) slots
-  float2* t2 = smem + lds_row(N);            // [p][16]
+  float2* row = smem;                        // layouts A / B, kR4kRow slots
+  float2* t2 = smem + kR4kRow;               // [p][16]
   float2* t3 = t2 + kR4kTw2;                 // [p][256]
   for (int e = tid; e < kR4kTw3; e += NT) {
     const int pp = e >> 8, k = e & 255;
@@ -95,11 +103,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void ro
     // pass 1 (NS 1): no twiddles, outputs tid 16 + r
     sdft<16, DIR>(v);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) row[lpad(tid * 16 + r)] = v[r];
+    for (int r = 0; r < 16; ++r) row[kR4kA * r + tid] = v[r];  // layout A
     __syncthreads();
     // pass 2 (NS 16): k = tid mod 16, twiddles w^r, r = 1..15, of m = 16 k
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = row[lpad(tid + 256 * r)];
+    for (int r = 0; r < 16; ++r) v[r] = row[kR4kA * k2 + (tid >> 4) + 16 * r];  // element tid + 256 r
     {
       float2 w[16];
       r4k_twiddles<DIR>(t2, k2, 16, w);
@@ -108,11 +116,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void ro
     sdft<16, DIR>(v);
     __syncthreads();  // every pass-2 load done before the in-place stores
 #pragma unroll
-    for (int r = 0; r < 16; ++r) row[lpad(st2 + 16 * r)] = v[r];
+    for (int r = 0; r < 16; ++r) row[st2 + 16 * r] = v[r];  // layout B
     __syncthreads();
     // pass 3 (NS 256): k = tid, twiddles of m = k; outputs tid + 256 r -> HBM
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = row[lpad(tid + 256 * r)];
+    for (int r = 0; r < 16; ++r) v[r] = row[tid + 256 * r];
     {
       float2 w[16];
       r4k_twiddles<DIR>(t3, tid, 256, w);

@@ -136,7 +136,13 @@ __device__ __forceinline__ void idft16_mid8(const float2* v, float2* y) {
 // SynthBlockArgs::win_flat): registers r = 4 .. 11 (rows m + 32 r) skip the multiply (exact)
 // PRIO: as synth_wave_kernel (1: issue priority 2 from the loop-top barrier to the swap-1
 // barrier)
-template <bool SPANS, bool XW, bool WFLAT = false, int PRIO = 0>
+// DEFER (round 5): block b's 8 output stores are issued at the top of block b + 1 (right
+// after its first barrier), from registers that stay live until block b + 1's pass B.  The
+// compiler makes any write to a register that is still the data source of an outstanding
+// buffer store wait for that store (vmcnt); with the stores at the end of their own block,
+// the next block's first register writes waited at the loop top for the stores it had just
+// issued (s_waitcnt vmcnt(0) there) — a store round trip per block, exposed.
+template <bool SPANS, bool XW, bool WFLAT = false, int PRIO = 0, bool DEFER = true>
 __global__ __launch_bounds__(kW5Threads) __attribute__((amdgpu_waves_per_eu(3)))
 void synth_wave512_kernel(SynthBlockArgs a) {
   constexpr int W = 448, DK = 8;  // keep = 256 rows = 8 register rows of 32
@@ -235,12 +241,53 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     });
   };
   prefetch(b_begin, std::false_type{});
+  // the first block's rows are complete before the loop: the loop top then has no load in
+  // flight on its entry path, and the wait-count merge at the loop head cannot turn into a
+  // wait for the previous block's (deferred) stores
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+
+  // output stores of one block: y[t] = y[t1a + 28 (t1b - 4)] of phase t0g + col2, t1b in [4, 12)
+  // (lanes t1a >= 28 hold no output: their offsets leave the descriptor's range; the whole
+  // offset is in the lane register — the buffer range check covers the lane offset, not a
+  // scalar offset, so a ragged last block drops its tail stores)
+  const int obase = (t1a < 28) ? (t1a * N + t0g + col2) * 8 : (int)0x80000000;
+  // a block's kept outputs end exactly at L_keep (t1a + 28 (t1b - 4) <= 223): for a whole
+  // block the row offsets t 28 N 8 can be scalar offsets and the lane offset register stays
+  // the same for the whole kernel (a store's address register rewritten while the store is
+  // in flight makes the compiler wait for it too); a ragged last block (nk < L_keep) keeps
+  // the whole offset in the range-checked lane register
+  auto out_nk = [&](int b) {
+    const int64_t ob = (a.block0 + b) * (int64_t)a.Lkeep;  // first kept output sample
+    const int64_t avail = a.out_limit - ob;
+    return (tmask(a.timing_mask) & 2) ? (int64_t)0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
+  };
+  auto store_block = [&](int b, const float2* yv) {
+    const int64_t nk = out_nk(b);
+    const __amdgpu_buffer_rsrc_t o = make_rsrc(opol + (a.block0 + b) * (int64_t)a.Lkeep, (uint32_t)nk * 8u);
+    if (nk == a.Lkeep) {  // uniform
+      static_for<0, 8>([&](auto t) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, yv[t]), o, (uint32_t)obase,
+                                              t * 28 * N * 8, kNtW5 ? 2 : 0);
+      });
+    } else {
+      int base = obase;
+      asm volatile("" : "+v"(base));
+      static_for<0, 8>([&](auto t) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, yv[t]), o,
+                                              (uint32_t)(base + t * 28 * N * 8), 0, kNtW5 ? 2 : 0);
+      });
+    }
+  };
+  [[maybe_unused]] float2 yprev[8];
 
 #pragma unroll 1
   for (int i = 0; i < nb; ++i) {
     const int b = b_begin + i;
     // every wave has read the previous block's swap-2 data (from all tiles)
     __syncthreads();
+    if constexpr (DEFER) {
+      if (i > 0) store_block(b - 1, yprev);  // uniform per workgroup
+    }
     if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(2);
     // ---- pass 1: taper, 16-point DFT over r, x w_512^{m f1}
     float2 v[16];
@@ -305,25 +352,19 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     static_for<0, 8>([&](auto k) { lds_pair2(lds + rd2 + 16 * k, v[2 * k], v[2 * k + 1]); });
     // ---- pass B: 16-point IDFT over f1 -> t1 = t1a + 28 t1b, only t1b in [4, 12) (the kept
     // outputs: L_ov = 112 N); stored as output sample (t1a + 28 (t1b - 4)) N + t0
-    float2 y[8];
-    idft16_mid8(v, y);
-    {
-      const int64_t ob = (a.block0 + b) * (int64_t)a.Lkeep;  // first kept output sample
-      const int64_t avail = a.out_limit - ob;
-      const int64_t nk = (tmask(a.timing_mask) & 2)
-                             ? 0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
-      const __amdgpu_buffer_rsrc_t o = make_rsrc(opol + ob, (uint32_t)nk * 8u);
-      // lanes t1a >= 28 hold no output: their offsets leave the descriptor's range
-      int base = (t1a < 28) ? (t1a * N + t0g + col2) * 8 : (int)0x80000000;
-      asm volatile("" : "+v"(base));
-      // (the whole offset in the lane register: the buffer range check covers the lane
-      // offset, not a scalar offset — a ragged last block must drop its tail stores)
-      static_for<0, 8>([&](auto t) {
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y[t]), o,
-                                              (uint32_t)(base + t * 28 * N * 8), 0, kNtW5 ? 2 : 0);
-      });
+    if constexpr (DEFER) {
+      // (the stored registers stay reserved until here — an empty use — so nothing else is
+      // allocated into them while their stores are in flight: no store wait in this block)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) asm volatile("" ::"v"(yprev[t]));
+      idft16_mid8(v, yprev);
+    } else {
+      float2 y[8];
+      idft16_mid8(v, y);
+      store_block(b, y);
     }
   }
+  if constexpr (DEFER) store_block(b_end - 1, yprev);  // the range's last block
 }
 
 bool synth_wave512_supported(const SynthBlockArgs& a) {
@@ -337,9 +378,12 @@ template <bool SPANS, bool XW, bool WFLAT = false>
 static hipError_t launch_w5(const SynthBlockArgs& a, hipStream_t s) {
   auto kern = synth_wave512_kernel<SPANS, XW, WFLAT>;
   if constexpr (kExperiments && XW && WFLAT) {
-    // (PFB_W5_PRIO=1: issue-priority A/B, experiments build only)
+    // (PFB_W5_PRIO=1: issue-priority A/B; PFB_W5_DEFER=0: stores at the end of their own
+    // block — experiments build only)
     static const int prio = knob("PFB_W5_PRIO") ? std::atoi(knob("PFB_W5_PRIO")) : 0;
     if (prio == 1) kern = synth_wave512_kernel<SPANS, XW, WFLAT, 1>;
+    static const bool nodefer = knob("PFB_W5_DEFER") && std::atoi(knob("PFB_W5_DEFER")) == 0;
+    if (nodefer) kern = synth_wave512_kernel<SPANS, XW, WFLAT, 0, false>;
   }
   hipError_t e = set_lds(kern, kW5LdsB);
   if (e != hipSuccess) return e;
