@@ -125,6 +125,7 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
   float2* zpol = ZOUT ? a.z + pol * a.z_pol_stride - a.z_row0 * N : nullptr;  // Z row k - z_row0
   LdsRows rows(smem, SH::RS);
   const float2* tw = smem + SH::TW_OFF;
+  vm_drain();
 #pragma unroll 1
   for (int64_t stp = st0; stp < st1; ++stp) {
     const int rel = (int)(stp - st0) * NEW;  // window row 0 of this step

@@ -278,6 +278,7 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
       const int q = i - (U - 1 - u) * DE;
       X[i] = ld(gidx(kfirst + (int64_t)u * NU, VARIANT == kBunton ? PW - 1 - q : q));
     }
+    vm_drain();  // (no store wait at the loop head)
 #pragma unroll 1
     for (int64_t j = j0; j < j1; j += U) {
       const int64_t k = s + (int64_t)NU * j;
@@ -312,6 +313,7 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
   v2f w[PW];
 #pragma unroll
   for (int p = 0; p < PW; ++p) w[p] = ld(gidx(kfirst, p));
+  vm_drain();  // (no store wait at the loop head)
 #pragma unroll 1
   for (int64_t j = j0; j < j1; ++j) {
     const int64_t k = s + (int64_t)NU * j;
@@ -478,6 +480,7 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges,
   v2f acc[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) acc[j] = v2f{0.f, 0.f};
+  vm_drain();  // (no store wait at the loop head)
 #pragma unroll 1
   for (int64_t qi = qw; qi < q1; qi += U) {
     // rows of this iteration -> ring, next iteration's rows -> registers

@@ -350,6 +350,7 @@ __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
   };
 #pragma unroll
   for (int k = 0; k < PF; ++k) load_row(min(q0 + k, q1 - 1), pf[k]);
+  vm_drain();
 #pragma unroll 1
   for (int64_t row = q0; row < q1; ++row) {
     float2 v[R];

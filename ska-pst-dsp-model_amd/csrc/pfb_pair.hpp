@@ -73,6 +73,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
 
+// s_waitcnt vmcnt(0) (gfx9 encoding: expcnt / lgkmcnt left at their maxima).  A software-
+// pipelined loop whose prologue issues the first loads should drain them before the loop:
+// the wait-count pass merges the loop head's entry path (those loads last in flight) with
+// the back edge (the prefetch loads, then the previous iteration's stores), and the merged
+// count makes the first use of the prefetched registers wait for the stores as well.
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // ------------------------------------------------------------------ LDS pair rows
 // Pair row q (rows 2q, 2q+1 of the batch) at base + q * rs, element i is one 16-byte
 // cpx2 slot {re_a, re_b, im_a, im_b}: ds_read_b128 / ds_write_b128, and the address is

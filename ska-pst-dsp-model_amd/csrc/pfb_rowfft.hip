@@ -91,6 +91,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void ro
     });
   };
   load_row(q0);
+  vm_drain();
   const int k2 = tid & 15;
   const int st2 = (tid >> 4) * 256 + k2;     // pass-2 output base (j / 16) 256 + k
 #pragma unroll 1
@@ -134,6 +135,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void ro
       t -= a.sds;
       while (t < 0) t += a.n_total;
     }
+    // (t is uniform, but the uniformity analysis loses it through the wrap loop: without the
+    // read-first-lane every store became a one-trip waterfall loop over the descriptor)
+    t = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)t >> 32)) << 32) |
+                  __builtin_amdgcn_readfirstlane((uint32_t)t));
     const __amdgpu_buffer_rsrc_t os = make_rsrc(out + t * N, (uint32_t)(N * 8));
     static_for<0, 16>([&](auto rv) {
       constexpr int r = decltype(rv)::value;

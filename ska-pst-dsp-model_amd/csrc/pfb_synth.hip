@@ -129,6 +129,7 @@ __global__ __launch_bounds__(NTPW) __attribute__((amdgpu_waves_per_eu(2))) void 
         });
       };
       prefetch(b_begin, std::false_type{});
+      vm_drain();
       const PairRegsIn<PF, R1> in{zv, win};
 #pragma unroll 1
       for (int b = b_begin; b < b_end; b += b_step) {

@@ -290,6 +290,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
   } else {
     prefetch(sch.block(0), std::false_type{});
   }
+  vm_drain();  // (no store wait at the loop head)
 
 #pragma unroll 1
   for (int i = 0; i < nb; ++i) {

@@ -241,10 +241,9 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     });
   };
   prefetch(b_begin, std::false_type{});
-  // the first block's rows are complete before the loop: the loop top then has no load in
-  // flight on its entry path, and the wait-count merge at the loop head cannot turn into a
-  // wait for the previous block's (deferred) stores
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  // (the first block's rows are complete before the loop: no wait for the previous block's
+  // stores at the loop head — vm_drain)
+  vm_drain();
 
   // output stores of one block: y[t] = y[t1a + 28 (t1b - 4)] of phase t0g + col2, t1b in [4, 12)
   // (lanes t1a >= 28 hold no output: their offsets leave the descriptor's range; the whole
