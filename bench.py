@@ -292,7 +292,9 @@ def traffic_for(workload, kernel, traffic):
     key = kernel_key(kernel)
     if key is None:
         return None, "no kernel name recorded for the dominant kernel class"
-    rec = (traffic.get(workload) or {}).get(key)
+    # (stored names are normalised the same way: "pfb::" qualifiers and all)
+    recs = {kernel_key(k) or k: v for k, v in (traffic.get(workload) or {}).items()}
+    rec = recs.get(key)
     if rec is None:
         return None, f"profiles/pmc_traffic.json has no {workload} record for {key}"
     return rec["bytes"], None

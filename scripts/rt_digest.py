@@ -2,7 +2,7 @@
 variants: the same input, any library build (PFB_HIP_LIB), one JSON line with the SHA-256
 of both buffers.  Variants that must be bit-identical print the same digests.
 
-    PFB_HIP_LIB=ska-pst-dsp-model_amd/lib/libpfb_hip_exp.so PFB_RT_ROWFFT_CONC=1 \\
+    PFB_HIP_LIB=ska-pst-dsp-model_amd/lib/libpfb_hip_exp.so PFB_W5_DEFER=0 \\
         python scripts/rt_digest.py --workload c3
 """
 import argparse

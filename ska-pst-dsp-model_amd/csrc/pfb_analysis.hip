@@ -368,8 +368,8 @@ struct FirLdsShape {
   static constexpr int CWP = CW + 1;                       // padded ring row (banks)
 };
 
-// PFD: iterations of input rows held in registers ahead of the ring (1, or 2: twice the
-// bytes in flight per workgroup, experiments A/B PFB_FIR_PF=2)
+// PFD: iterations of input rows held in registers ahead of the ring (1; 2 — twice the bytes
+// in flight per workgroup — was measured no faster in rounds 1 and 4 and its knob retired)
 template <int PW, int DE, int NU, int VARIANT, int PFD = 1>
 __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges, int cs, int xcd) {
   using SH = FirLdsShape<NU, DE>;
@@ -547,16 +547,6 @@ static hipError_t launch_fir_lds_t(const AnalysisArgs& a, hipStream_t s) {
   static const bool no_zalign = knob("PFB_FIR_ZALIGN") && std::atoi(knob("PFB_FIR_ZALIGN")) == 0;
   const int cs = (a.variant == kPadded && a.z && !no_zalign) ? a.N - 1 : 0;
   static const int xcd = knob("PFB_FIR_LDS_XCD") ? std::atoi(knob("PFB_FIR_LDS_XCD")) : 1;
-  if constexpr (kExperiments) {
-    static const bool pf2 = knob("PFB_FIR_PF") && std::atoi(knob("PFB_FIR_PF")) == 2;
-    if (pf2) {
-      if (a.variant == kBunton)
-        hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kBunton, 2>), grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);
-      else
-        hipLaunchKernelGGL((fir_lds_kernel<PW, DE, NU, kPadded, 2>), grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);
-      return hipGetLastError();
-    }
-  }
   // (launch_kernel: timed by the profiler's armed events like every other single launch)
   if (a.variant == kBunton)
     return launch_kernel(fir_lds_kernel<PW, DE, NU, kBunton>, grid, dim3(NT), 0, s, a, (int)ranges, cs, xcd);

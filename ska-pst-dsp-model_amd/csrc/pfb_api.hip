@@ -1661,113 +1661,24 @@ static pfb_status roundtrip_run(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, c
   zkey_clear(ps);  // phase 0 reuses Z
   if (fuse) {
     float2* Z = ps->Z.as<float2>();
-    static const int conc = pfb::knob("PFB_RT_CONC") ? std::atoi(pfb::knob("PFB_RT_CONC")) : 1;
-    const int64_t C = std::min<int64_t>(std::max(conc, 1), B);
-    // generic (N > 256) path: the row FFT (Z -> channelised rows) and the synthesis (Z ->
-    // output) both read Z and are independent, so the row FFT may run on the analysis
-    // plan's stream beside the synthesis (PFB_RT_ROWFFT_CONC=1, experiments A/B)
-    static const bool rowfft_conc = pfb::knob("PFB_RT_ROWFFT_CONC") && std::atoi(pfb::knob("PFB_RT_ROWFFT_CONC")) == 1;
-    if (!pa->fused && rowfft_conc) {
-      pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0,
-                                   nullptr, zblk, nullptr, 1);
-      if (st != PFB_OK) return st;
-      if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));
-      while (pa->events.size() < 2) {
-        hipEvent_t e;
-        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        pa->events.push_back(e);
-      }
-      HIPCHK(hipEventRecord(pa->events[0], s));
-      HIPCHK(hipStreamWaitEvent(pa->aux, pa->events[0], 0));
-      st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, pa->aux, Z, zrows * pa->N, z0, 0, nullptr,
-                        zblk, nullptr, 2);
-      if (st != PFB_OK) return st;
-      st = synthesis_blocks(ps, Z + (off - z0) * pa->N, zrows * pa->N, 0, B, (float2*)out, out_ps, olen, s,
-                            zblk);
-      if (st != PFB_OK) return st;
-      HIPCHK(hipEventRecord(pa->events[1], pa->aux));
-      HIPCHK(hipStreamWaitEvent(s, pa->events[1], 0));
-      return PFB_OK;
-    }
-    // generic (N > 256) path in chunks of synthesis blocks (PFB_RT_C3_CHUNKS=n, experiments
-    // A/B): FIR -> row FFT -> synthesis per chunk, so each chunk's stage-1 rows are read by
-    // the row FFT and the synthesis shortly after the FIR wrote them (Infinity-Cache
-    // resident, profiles/r04_v1_mall_probe.jsonl).  Z row t comes from FIR row
-    // (t + sds) mod K (padded circular shift), so the rows of Z [z_lo, z_hi) are FIR rows
-    // [z_lo + sds, z_hi + sds), the part past K wrapping to [0, ...).
-    static const int c3_chunks = pfb::knob("PFB_RT_C3_CHUNKS") ? std::atoi(pfb::knob("PFB_RT_C3_CHUNKS")) : 0;
-    if (!pa->fused && c3_chunks > 1 && z0 == 0 && !zblk && B >= c3_chunks) {
-      const int64_t sds = pa->variant == pfb::kPadded ? pa->sds : 0;
-      int64_t zdone = 0;
-      for (int64_t c = 0; c < c3_chunks; ++c) {
-        const int64_t b0 = B * c / c3_chunks, b1 = B * (c + 1) / c3_chunks;
-        const int64_t need = (c == c3_chunks - 1) ? K : std::min(K, off + b1 * ps->keep + 2 * (int64_t)ps->Ov);
-        if (need > zdone) {
-          const int64_t k0 = zdone + sds, k1 = need + sds;
-          pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, std::min(k0, K), std::min(k1, K), K, s, Z,
-                                       zrows * pa->N, 0, 0, nullptr, 0, nullptr, 1);
-          if (st != PFB_OK) return st;
-          if (k1 > K) {  // the wrapped tail of Z: FIR rows [max(k0 - K, 0), k1 - K)
-            st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, std::max<int64_t>(k0 - K, 0), k1 - K, K, s, Z,
-                              zrows * pa->N, 0, 0, nullptr, 0, nullptr, 1);
-            if (st != PFB_OK) return st;
-          }
-          st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, zdone, need, K, s, Z, zrows * pa->N, 0, 0, nullptr,
-                            0, nullptr, 2);
-          if (st != PFB_OK) return st;
-          zdone = need;
-        }
-        pfb_status st = synthesis_blocks(ps, Z + (off + b0 * ps->keep) * pa->N, zrows * pa->N, b0, b1 - b0,
-                                         (float2*)out, out_ps, olen, s, 0);
-        if (st != PFB_OK) return st;
-      }
-      return PFB_OK;
-    }
-    if (C <= 1 || !zblk) {
-      // (generic N > 256 path: the FIR and the row FFT as two calls on the stream — the same
-      // two launches as one call, each then timed alone by the profiler)
-      pfb_status st = PFB_OK;
-      if (!pa->fused) {
+    // (retired round 5, measured slower twice: the row FFT on a second stream beside the
+    // synthesis, Infinity-Cache chunking of the generic path and chunked analysis/synthesis
+    // concurrency — profiles/HISTORY.md)
+    // (generic N > 256 path: the FIR and the row FFT as two calls on the stream — the same
+    // two launches as one call, each then timed alone by the profiler)
+    pfb_status st = PFB_OK;
+    if (!pa->fused) {
+      st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0, nullptr, zblk,
+                        nullptr, 1);
+      if (st == PFB_OK)
         st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0, nullptr, zblk,
-                          nullptr, 1);
-        if (st == PFB_OK)
-          st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0, nullptr, zblk,
-                            nullptr, 2);
-      } else {
-        st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0, nullptr, zblk);
-      }
-      if (st != PFB_OK) return st;
-      return synthesis_blocks(ps, Z + (off - z0) * pa->N, zrows * pa->N, 0, B, (float2*)out, out_ps,
-                              olen, s, zblk);
+                          nullptr, 2);
+    } else {
+      st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, 0, K, K, s, Z, zrows * pa->N, z0, 0, nullptr, zblk);
     }
-    // (experiments) C chunks of blocks: the analysis of chunk c+1 on the aux stream runs
-    // beside the synthesis of chunk c (rows in whole 16-row steps from `off`)
-    if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));
-    while ((int64_t)pa->events.size() < C + 2) {
-      hipEvent_t e;
-      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      pa->events.push_back(e);
-    }
-    HIPCHK(hipEventRecord(pa->events[0], s));
-    HIPCHK(hipStreamWaitEvent(pa->aux, pa->events[0], 0));
-    int64_t ra = 0;
-    for (int64_t c = 0; c < C; ++c) {
-      const int64_t b_lo = B * c / C, b_hi = B * (c + 1) / C;
-      int64_t rb = (c == C - 1) ? K : off + ((b_hi * ps->keep + 2 * (int64_t)ps->Ov + 15) / 16) * 16;
-      rb = std::max(ra, std::min(K, rb));
-      pfb_status st = analysis_run(pa, x, in_ps, n_dat, y, chan_ps, ra, rb, K, pa->aux, Z, zrows * pa->N,
-                                   z0, 0, nullptr, zblk);
-      if (st != PFB_OK) return st;
-      ra = rb;
-      HIPCHK(hipEventRecord(pa->events[1 + c], pa->aux));
-      HIPCHK(hipStreamWaitEvent(s, pa->events[1 + c], 0));
-      st = synthesis_blocks(ps, Z + (off - z0 + b_lo * ps->keep) * pa->N, zrows * pa->N, b_lo, b_hi - b_lo,
-                            (float2*)out, out_ps, olen, s, zblk);
-      if (st != PFB_OK) return st;
-    }
-    HIPCHK(hipEventRecord(pa->events[1 + C], pa->aux));
-    HIPCHK(hipStreamWaitEvent(s, pa->events[1 + C], 0));
-    return PFB_OK;
+    if (st != PFB_OK) return st;
+    return synthesis_blocks(ps, Z + (off - z0) * pa->N, zrows * pa->N, 0, B, (float2*)out, out_ps,
+                            olen, s, zblk);
   }
 
   if (!pa->aux) HIPCHK(hipStreamCreateWithFlags(&pa->aux, hipStreamNonBlocking));

@@ -314,13 +314,13 @@ __device__ __forceinline__ void run_rest(const LdsRows& lds, const Last& last, c
 // columns in registers, and loads row r + 1 into registers while it transforms row r.
 // (The one-shot kernel re-read the 32 KB table from L2 for every one of the 73 400 C3
 // rows and waited for each row's loads with nothing in flight.)
-// PF: rows prefetched ahead (1, or 2 with 32 more VGPRs: 64 KB in flight per workgroup).
-// HT: half twiddle table (HalfTw: N / 2 entries, 17 KB less LDS per workgroup).
+// (Two rows prefetched ahead and a half twiddle table were measured no faster, rounds 2
+// and 4, and retired.)
 template <int N>
-constexpr size_t row_fft_persist_lds(bool ht) {
-  return ((size_t)RowShape<N>::RS + tw_slots(ht ? N / 2 : N)) * sizeof(float2);
+constexpr size_t row_fft_persist_lds() {
+  return ((size_t)RowShape<N>::RS + tw_slots(N)) * sizeof(float2);
 }
-template <int N, int DIR, bool PERM, bool GAIN, int PF = 1, bool HT = false>
+template <int N, int DIR, bool PERM, bool GAIN>
 __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
   static_assert(RowShape<N>::ROWS == 1, "one row per workgroup");
   constexpr int R = FirstPassOf<N, 1, NT>::R, NB = N / R;
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
   const int tid = threadIdx.x;
   LdsRows rows(smem, RowShape<N>::RS);
   float2* tw = smem + RowShape<N>::RS;
-  for (int m = tid; m < (HT ? N / 2 : N); m += NT) tw[tw_slot(m)] = a.tw[m];
+  for (int m = tid; m < N; m += NT) tw[tw_slot(m)] = a.tw[m];
   const float2* in = a.in + pol * a.in_pol_stride;
   int col[R];
   float g[R];
@@ -343,24 +343,19 @@ __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
     col[r] = PERM ? a.perm[i] : i;
     g[r] = GAIN ? a.cgain[col[r]] : 1.f;
   }
-  float2 pf[PF][R];
-  auto load_row = [&](int64_t row, float2* d) {
+  float2 pf[R];
+  auto load_row = [&](int64_t row) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) d[r] = ld_nt<kNtlRow>(in + row * N + col[r]);
+    for (int r = 0; r < R; ++r) pf[r] = ld_nt<kNtlRow>(in + row * N + col[r]);
   };
-#pragma unroll
-  for (int k = 0; k < PF; ++k) load_row(min(q0 + k, q1 - 1), pf[k]);
+  load_row(q0);
   vm_drain();
 #pragma unroll 1
   for (int64_t row = q0; row < q1; ++row) {
     float2 v[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[r] = GAIN ? cscale(pf[0][r], g[r]) : pf[0][r];
-#pragma unroll
-    for (int k = 0; k + 1 < PF; ++k)
-#pragma unroll
-      for (int r = 0; r < R; ++r) pf[k][r] = pf[k + 1][r];
-    load_row(min(row + PF, q1 - 1), pf[PF - 1]);  // unconditional: past the end re-reads the last row
+    for (int r = 0; r < R; ++r) v[r] = GAIN ? cscale(pf[r], g[r]) : pf[r];
+    load_row(min(row + 1, q1 - 1));  // unconditional: past the end re-reads the last row
     __syncthreads();  // tables / the previous row's last pass done with the LDS row
     // first pass (radix R, stride 1): no twiddles, outputs j R + r
     sdft<R, DIR>(v);
@@ -369,8 +364,7 @@ __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
     __syncthreads();
     RowStore st{a.out + pol * a.out_pol_stride, row, a.n_rows, N, a.sds, a.remap, a.scale,
                 a.row_base, a.n_total, a.zs};
-    if constexpr (HT) run_rest<N, DIR>(rows, st, HalfTw{tw, ilog2(N / 2)}, tid, typename FFTPlan<N>::type{});
-    else run_rest<N, DIR>(rows, st, (const float2*)tw, tid, typename FFTPlan<N>::type{});
+    run_rest<N, DIR>(rows, st, (const float2*)tw, tid, typename FFTPlan<N>::type{});
   }
 }
 

@@ -313,21 +313,6 @@ __host__ __device__ constexpr int high_bit(int r) {
   while (2 * h <= r) h *= 2;
   return h;
 }
-// Half table (the persistent 4096-point row FFT): entries m < H = N / 2 only, the upper
-// half from e^{-2 pi i (m + H) / N} = -e^{-2 pi i m / N} (a sign flip, exact) — half the LDS,
-// so one more workgroup fits per CU
-struct HalfTw {
-  const float2* p;
-  int h_log2;  // H = 2^h_log2
-};
-template <int DIR>
-__device__ __forceinline__ float2 table_tw(const HalfTw& t, int m) {
-  float2 w = t.p[tw_slot(m & ((1 << t.h_log2) - 1))];
-  const uint32_t sg = ((uint32_t)m >> t.h_log2) << 31;  // m < N: bit h_log2 is the half
-  w.x = __uint_as_float(__float_as_uint(w.x) ^ sg);
-  w.y = __uint_as_float(__float_as_uint(w.y) ^ (DIR > 0 ? sg ^ 0x80000000u : sg));
-  return w;
-}
 template <int R, int DIR, class TW>
 __device__ __forceinline__ void twiddle_powers(const TW& tw, int m, float2 (&w)[R]) {
   static_for<1, R>([&](auto rv) {

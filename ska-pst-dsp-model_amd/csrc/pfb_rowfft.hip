@@ -149,11 +149,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void ro
 }
 
 template <int DIR, bool PERM, bool GAIN>
-static hipError_t launch_row_fft4096(const RowFftArgs& r, int n_pol, hipStream_t s, int per_cu, int wgs_override) {
+static hipError_t launch_row_fft4096(const RowFftArgs& r, int n_pol, hipStream_t s, int per_cu) {
   auto kern = row_fft4096_kernel<DIR, PERM, GAIN>;
   hipError_t e = set_lds(kern, kR4kLds);
   if (e != hipSuccess) return e;
-  const int64_t wgs = wgs_override > 0 ? wgs_override : (int64_t)cu_count() * per_cu;
+  const int64_t wgs = (int64_t)cu_count() * per_cu;
   dim3 grid((unsigned)std::max<int64_t>(1, wgs / n_pol), (unsigned)n_pol);
   return launch_kernel(kern, grid, dim3(NT), kR4kLds, s, r);
 }
@@ -165,15 +165,9 @@ static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s
     // persistent workgroups (row_fft_persist_kernel) once there are several rows per
     // resident workgroup; PFB_ROWFFT_PERSIST=0: one workgroup per row (A/B)
     static const bool off = knob("PFB_ROWFFT_PERSIST") && std::atoi(knob("PFB_ROWFFT_PERSIST")) == 0;
-    // (PFB_ROWFFT_HT=1: half twiddle table, experiments A/B)
-    static const bool ht = kExperiments && knob("PFB_ROWFFT_HT") && std::atoi(knob("PFB_ROWFFT_HT")) == 1;
-    const size_t bytes = row_fft_persist_lds<N>(ht);
+    const size_t bytes = row_fft_persist_lds<N>();
     const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / bytes);
-    int64_t wgs = (int64_t)cu_count() * per_cu;
-    // (PFB_ROWFFT_WGS: fewer persistent workgroups, so the row FFT can share the chip with
-    // a concurrent synthesis — experiments A/B)
-    static const int env_wgs = knob("PFB_ROWFFT_WGS") ? std::atoi(knob("PFB_ROWFFT_WGS")) : 0;
-    if (env_wgs > 0) wgs = env_wgs;
+    const int64_t wgs = (int64_t)cu_count() * per_cu;
     // the explicit-pass kernel with per-pass twiddle tables (PFB_ROWFFT_4K=0: the generic
     // persistent kernel; PFB_ROWFFT_WPC: its workgroups per CU, default the 3 LDS allows —
     // experiments A/B)
@@ -181,15 +175,9 @@ static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s
     static const int wpc = knob("PFB_ROWFFT_WPC") ? std::atoi(knob("PFB_ROWFFT_WPC")) : 0;
     const int per_cu4 = wpc > 0 ? wpc : (int)std::max<size_t>(1, std::min<size_t>(3, (160 * 1024) / kR4kLds));
     if (!off && k4 && r.zs == 0 && r.n_rows >= 4 * (int64_t)cu_count() * per_cu4)
-      return launch_row_fft4096<DIR, PERM, GAIN>(r, n_pol, s, per_cu4, env_wgs);
+      return launch_row_fft4096<DIR, PERM, GAIN>(r, n_pol, s, per_cu4);
     if (!off && r.n_rows >= 4 * wgs) {
-      // (PFB_ROWFFT_PF=2: two rows prefetched ahead, experiments A/B)
-      auto kern = row_fft_persist_kernel<N, DIR, PERM, GAIN, 1>;
-      if constexpr (kExperiments) {
-        static const bool pf2 = knob("PFB_ROWFFT_PF") && std::atoi(knob("PFB_ROWFFT_PF")) == 2;
-        if (pf2) kern = row_fft_persist_kernel<N, DIR, PERM, GAIN, 2>;
-        if (ht) kern = row_fft_persist_kernel<N, DIR, PERM, GAIN, 1, true>;
-      }
+      auto kern = row_fft_persist_kernel<N, DIR, PERM, GAIN>;
       hipError_t e = set_lds(kern, bytes);
       if (e != hipSuccess) return e;
       dim3 grid((unsigned)std::max<int64_t>(1, wgs / n_pol), (unsigned)n_pol);

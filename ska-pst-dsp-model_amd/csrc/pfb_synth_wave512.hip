@@ -377,10 +377,7 @@ template <bool SPANS, bool XW, bool WFLAT = false>
 static hipError_t launch_w5(const SynthBlockArgs& a, hipStream_t s) {
   auto kern = synth_wave512_kernel<SPANS, XW, WFLAT>;
   if constexpr (kExperiments && XW && WFLAT) {
-    // (PFB_W5_PRIO=1: issue-priority A/B; PFB_W5_DEFER=0: stores at the end of their own
-    // block — experiments build only)
-    static const int prio = knob("PFB_W5_PRIO") ? std::atoi(knob("PFB_W5_PRIO")) : 0;
-    if (prio == 1) kern = synth_wave512_kernel<SPANS, XW, WFLAT, 1>;
+    // (PFB_W5_DEFER=0: stores at the end of their own block — experiments build only)
     static const bool nodefer = knob("PFB_W5_DEFER") && std::atoi(knob("PFB_W5_DEFER")) == 0;
     if (nodefer) kern = synth_wave512_kernel<SPANS, XW, WFLAT, 0, false>;
   }
