@@ -63,7 +63,7 @@ struct ColMajorLds {
 // column (AnalysisArgs::zblk) for the synthesis wave kernel.
 // Streaming analysis of step range w of nw (steps of T rows from row0) for polarisation
 // pol.
-template <int N, int P, int NU, int DE, int ZOUT, bool LCBF, bool GS>
+template <int N, int P, int NU, int DE, int ZOUT, bool LCBF, int GS>
 __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int pol, int w, int nw) {
   using SH = StreamShape<N, P, NU, DE>;
   constexpr int M = SH::M, PE = SH::PE, QS = SH::QS, T = SH::T, NEW = SH::NEW, WIN = SH::WIN;
@@ -196,39 +196,36 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
     if constexpr (LCBF) {
       const LcbfRowStore st = LcbfRowStore::rows(opol, k0, T, a.row0, a.K, a.lcbf_scale);
       block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
-    } else if constexpr (GS) {
-      if (a.out_rs == 1 && a.sel_n == 0) {
-        // channel-major (a cascade's stage-2 series): the last pass lands in LDS by
-        // channel, then each 8-lane group writes one channel's T = 16 consecutive
-        // samples as 8 x 16 B (one 128-B run) instead of 16 scattered 8-B stores
-        static_assert(N * (T + 1) <= T * SH::RS, "channel-major staging exceeds the LDS rows");
-        const ColMajorLds<T> cm{smem};
-        block_fft<N, -1, T, NT>(rows, cm, rows, tw, c);
-        __syncthreads();
-        const int hi = (int)min(max(a.K - k0, (int64_t)0), (int64_t)T);
-        const int lo = (int)min(max(a.row0 - k0, (int64_t)0), (int64_t)T);
-        const __amdgpu_buffer_rsrc_t r =
-            make_rsrc(opol + k0, hi > 0 ? (uint32_t)(((int64_t)(N - 1) * a.out_cs + hi) * 8) : 0u);
-        static_for<0, (T / 2) * N / NT>([&](auto iv) {
-          const int idx = c + decltype(iv)::value * NT;
-          const int ch = idx / (T / 2), r0 = 2 * (idx % (T / 2));
-          const float2 v0 = cscale(cm.load(r0, ch), (float)N), v1 = cscale(cm.load(r0 + 1, ch), (float)N);
-          const uint32_t off = (uint32_t)((ch * a.out_cs + r0) * 8);
-          if (r0 >= lo && r0 + 1 < hi) {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{v0.x, v0.y, v1.x, v1.y}), r, off, 0,
-                                                   kAuxColMajor);
-          } else {
-            if (r0 >= lo && r0 < hi)
-              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v0), r, off, 0, kAuxColMajor);
-            if (r0 + 1 >= lo && r0 + 1 < hi)
-              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v1), r, off + 8, 0, kAuxColMajor);
-          }
-        });
-      } else {
-        const StridedRowStore st = StridedRowStore::rows(opol, k0, T, a.row0, a.K, a.out_rs, a.out_cs,
-                                                         a.sel_split, a.sel_shift, a.sel_n, N, (float)N);
-        block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
-      }
+    } else if constexpr (GS == 2) {
+      // channel-major (a cascade's stage-2 series, out_rs = 1, no chomp): the last pass
+      // lands in LDS by channel, then each 8-lane group writes one channel's T = 16
+      // consecutive samples as 8 x 16 B (one 128-B run) instead of 16 scattered 8-B stores.
+      // The launch's first and last rows are even (launch_stream checks), so a row pair is
+      // valid or not as a whole: one store per pair, always issued, invalid pairs sent out
+      // of the descriptor's range.  (Stores under a branch made the count path-dependent,
+      // and the loop-end wait for the next step's rows then waited for the stores as well;
+      // the strided store (GS 1) is a kernel of its own for the same reason: a different
+      // store count per step.)
+      static_assert(N * (T + 1) <= T * SH::RS, "channel-major staging exceeds the LDS rows");
+      const ColMajorLds<T> cm{smem};
+      block_fft<N, -1, T, NT>(rows, cm, rows, tw, c);
+      __syncthreads();
+      const int hi = (int)min(max(a.K - k0, (int64_t)0), (int64_t)T);
+      const int lo = (int)min(max(a.row0 - k0, (int64_t)0), (int64_t)T);
+      const __amdgpu_buffer_rsrc_t r =
+          make_rsrc(opol + k0, hi > 0 ? (uint32_t)(((int64_t)(N - 1) * a.out_cs + hi) * 8) : 0u);
+      static_for<0, (T / 2) * N / NT>([&](auto iv) {
+        const int idx = c + decltype(iv)::value * NT;
+        const int ch = idx / (T / 2), r0 = 2 * (idx % (T / 2));
+        const float2 v0 = cscale(cm.load(r0, ch), (float)N), v1 = cscale(cm.load(r0 + 1, ch), (float)N);
+        const uint32_t off = (r0 >= lo && r0 + 1 < hi) ? (uint32_t)((ch * a.out_cs + r0) * 8) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{v0.x, v0.y, v1.x, v1.y}), r, off, 0,
+                                               kAuxColMajor);
+      });
+    } else if constexpr (GS == 1) {
+      const StridedRowStore st = StridedRowStore::rows(opol, k0, T, a.row0, a.K, a.out_rs, a.out_cs,
+                                                       a.sel_split, a.sel_shift, a.sel_n, N, (float)N);
+      block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
     } else {
       const BufRowStore st = BufRowStore::rows(opol, k0, T, a.row0, a.K, N, (float)N);
       block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
@@ -240,7 +237,7 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
   }
 }
 
-template <int N, int P, int NU, int DE, int ZOUT, bool LCBF = false, bool GS = false>
+template <int N, int P, int NU, int DE, int ZOUT, bool LCBF = false, int GS = 0>
 __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
   analysis_stream_body<N, P, NU, DE, ZOUT, LCBF, GS>(a, blockIdx.y, xcd_tile(blockIdx.x, gridDim.x), gridDim.x);
 }

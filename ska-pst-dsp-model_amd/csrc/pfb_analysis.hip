@@ -653,10 +653,13 @@ static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
               : a.z ? (a.zblk == 4   ? analysis_stream_kernel<N, P, NU, DE, 4>
                        : a.zblk == 2 ? analysis_stream_kernel<N, P, NU, DE, 2>
                                      : analysis_stream_kernel<N, P, NU, DE, 1>)
-              : a.out_rs > 0 ? analysis_stream_kernel<N, P, NU, DE, 0, false, true>
-                             : analysis_stream_kernel<N, P, NU, DE, 0>;
+              : a.out_rs == 1 && a.sel_n == 0 ? analysis_stream_kernel<N, P, NU, DE, 0, false, 2>
+              : a.out_rs > 0                  ? analysis_stream_kernel<N, P, NU, DE, 0, false, 1>
+                                              : analysis_stream_kernel<N, P, NU, DE, 0>;
+  // channel-major stores go out in row pairs: the launch's rows must start and end even
+  if (!LCBF && !a.z && a.out_rs == 1 && a.sel_n == 0 && ((a.row0 & 1) || (a.K & 1))) return hipErrorInvalidValue;
   // the carry (pre) is read only in each workgroup's first WIN-row window prologue: every
-  // pad sample must lie inside the first window (the caller's B <= P N guard)
+  // pad sample must lie inside the first window (the caller checks B <= WIN N)
   if (a.pre && (a.pad < 0 || a.pad > (int64_t)SH::WIN * N)) return hipErrorInvalidValue;
   hipError_t e = set_lds(kern, SH::lds_bytes);
   if (e != hipSuccess) return e;

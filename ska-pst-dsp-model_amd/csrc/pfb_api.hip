@@ -646,10 +646,16 @@ static pfb_status filterbank_exec(pfb_analysis_plan* p, const pfb_cf32* in, int6
       if (Kt > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld rows",
                                 (long long)cap, (long long)Kt);
       const int64_t M = p->M, PN = (int64_t)p->P * p->N;
-      if (B <= PN) {
+      // the streaming kernel's register window: DE (16 / NU) new rows per step + P (its first
+      // window holds every carried sample a workgroup's rows read when B fits in it —
+      // launch_stream checks the same bound)
+      const int64_t win = ((int64_t)p->de * (16 / p->nu) + p->P) * p->N;
+      if (B <= win) {
         // ONE launch: the streaming kernel reads the carried samples through a second
         // descriptor in its first window (AnalysisArgs::pre) — no stitched rows, no copies
-        // before it; then the new carry (stream order: after the kernel read the old one)
+        // before it; then the new carry (stream order: after the kernel read the old one).
+        // (Round 5: the bound was P N; a cascade's stage-2 carry of up to P N + NU M samples
+        // per series then took the stitched path — two copies and a small launch per call.)
         pfb_status st = analysis_run(p, (const float2*)in, in_ps, n_in, (float2*)out, out_ps, 0, Kt, K, s,
                                      nullptr, 0, 0, B, lay, 0, p->carry.as<float2>());
         if (st != PFB_OK) return st;
@@ -662,7 +668,8 @@ static pfb_status filterbank_exec(pfb_analysis_plan* p, const pfb_cf32* in, int6
         p->buffered = std::max<int64_t>(nb, 0);
         return PFB_OK;
       }
-      const int64_t k_split = std::min(Kt, (B + M - 1) / M);
+      // (even: a channel-major strided launch stores row pairs; Kt is a multiple of nu)
+      const int64_t k_split = std::min(Kt, (((B + M - 1) / M) + 1) & ~(int64_t)1);
       if (k_split > 0) {
         const int64_t L = std::min(total, (k_split - 1) * M + PN);
         HIPCHK(p->work.ensure((size_t)p->n_pol * L * sizeof(float2)));

@@ -422,6 +422,37 @@ def test_filterbank_stream_carry_in_place(gpu, os_, tpc):
     assert torch.equal(streamed, whole[:, :, :streamed.shape[2]])
 
 
+@pytest.mark.parametrize("os_", ["8/7", "4/3"])
+def test_filterbank_stream_long_carry_one_launch(gpu, os_):
+    """Carries longer than P N (up to P N + NU M samples: the nu-trimmed rows' samples stay
+    buffered, FilterBank.m:93-104,119-126) are read through the streaming kernel's carry
+    descriptor in its first register window (DE 16/NU + P rows) — one launch per call,
+    no stitched rows (round 5; the bound was P N).  Every call must equal the one-shot
+    analysis bit for bit, and the chunk lengths are chosen so that such carries occur."""
+    import torch
+    pfb = _pfb()
+    taps = pfb.design_PFB_FIR_filter(256, os_, 12)
+    cfg = dict(analysis_function="polyphase_analysis", filt_coeff=taps, channels=256,
+               os_factor=os_)
+    fb = pfb.FilterBank(cfg)
+    nu, de = (8, 7) if os_ == "8/7" else (4, 3)
+    M, P = 256 * de // nu, -(-len(taps) // 256)
+    chunks = [50000 + 977 * i for i in range(12)]
+    x = torch.from_numpy(_noise(np.random.default_rng(44), (1, 1, sum(chunks)))).cuda()
+    parts, a, long_carries = [], 0, 0
+    for n in chunks:
+        b = fb.buffered_samples
+        if P * 256 < b <= (de * 16 // nu + P) * 256:
+            long_carries += 1
+        fb, y = fb.execute(x[:, :, a:a + n])
+        parts.append(y)
+        a += n
+    assert long_carries >= 2, long_carries
+    streamed = torch.cat(parts, dim=2)
+    whole = pfb.polyphase_analysis(x, taps, 256, os_)
+    assert torch.equal(streamed, whole[:, :, :streamed.shape[2]])
+
+
 def test_filterbank_stream_padded(gpu):
     """Streaming FilterBank on the SKA-Mid padded (commutator) analysis: 4096 channels,
     100 353 two-stage taps, 8/7 (FilterBank.m:85-126 calling polyphase_analysis_padded).
