@@ -381,7 +381,14 @@ static hipError_t launch_w5(const SynthBlockArgs& a, hipStream_t s) {
     static const bool nodefer = knob("PFB_W5_DEFER") && std::atoi(knob("PFB_W5_DEFER")) == 0;
     if (nodefer) kern = synth_wave512_kernel<SPANS, XW, WFLAT, 0, false>;
   }
-  hipError_t e = set_lds(kern, kW5LdsB);
+  // (PFB_W5_LDS_PAD: extra LDS per workgroup, so fewer workgroups fit a CU — the occupancy
+  // slope, experiments build only)
+  size_t lds = kW5LdsB;
+  if constexpr (kExperiments) {
+    static const int pad = knob("PFB_W5_LDS_PAD") ? std::atoi(knob("PFB_W5_LDS_PAD")) : 0;
+    if (pad > 0) lds += (size_t)pad;
+  }
+  hipError_t e = set_lds(kern, lds);
   if (e != hipSuccess) return e;
   const int groups = a.N / kW5Cols;
   // resident workgroups: 3 per CU; ranges so that the grid is about two rounds of them
@@ -391,7 +398,7 @@ static hipError_t launch_w5(const SynthBlockArgs& a, hipStream_t s) {
   if (env_r > 0) ranges = env_r;
   ranges = std::min(ranges, a.n_blocks);
   dim3 grid((unsigned)(groups * ranges), (unsigned)a.n_pol);
-  return launch_kernel(kern, grid, dim3(kW5Threads), kW5LdsB, s, a);
+  return launch_kernel(kern, grid, dim3(kW5Threads), lds, s, a);
 }
 
 hipError_t launch_synth_wave512(const SynthBlockArgs& a, hipStream_t s) {
