@@ -16,5 +16,11 @@ timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.json 
 rc=$?; echo "bench rc=$rc"; if [ $rc -ne 0 ]; then tail -5 gpurun_out/bench.err; exit $rc; fi
 if [ -n "${AB:-}" ]; then
   ROUNDS=${ROUNDS:-2} timeout -k 10 900 bash scripts/gpu_c3_ab.sh $AB > gpurun_out/c3_ab.log 2>&1
-  rc=$?; echo "c3 ab rc=$rc"; tail -3 gpurun_out/c3_ab.log; exit $rc
+  rc=$?; echo "c3 ab rc=$rc"; tail -3 gpurun_out/c3_ab.log; [ $rc -ne 0 ] && exit $rc
+fi
+if [ -n "${PROF:-}" ]; then
+  rm -rf gpurun_out/prof_bench
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o bench -- \
+      python bench.py --steps 20 --warmup 3 > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err
+  rc=$?; echo "bench under rocprof rc=$rc"; exit $rc
 fi

@@ -1,5 +1,6 @@
 """A few steps of one workload for rocprofv3 --pmc passes (scripts/gpu_pmc_r05.sh):
-c2 = the fused C2 round trip (bench.py's step), c2syn = the standalone C2 synthesis
+c2 = the fused C2 round trip (bench.py's step), c4 = the same for a dual-pol unit (bench.py
+--gpus N > 1), c2syn = the standalone C2 synthesis
 (SynthesisPlan.execute of an HBM-resident channelised product), c3 = the SKA-Mid round trip.
 Every kernel name then maps to one workload in profiles/pmc_traffic.json."""
 import argparse
@@ -14,7 +15,7 @@ sys.path[:0] = [os.path.join(REPO, "ska-pst-dsp-model_amd"), REPO]
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("c2", "c2syn", "c3"), required=True)
+    ap.add_argument("--workload", choices=("c2", "c4", "c2syn", "c3"), required=True)
     ap.add_argument("--steps", type=int, default=3)
     args = ap.parse_args()
     import torch
@@ -27,11 +28,12 @@ def main():
     else:
         taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
         N, nf, ov, var, n = 256, 256, 48, "polyphase_analysis", 1 << 24
-    x = (torch.complex(torch.randn((1, n), device=dev, generator=g),
-                       torch.randn((1, n), device=dev, generator=g)) / np.sqrt(2)).to(torch.complex64)
-    ana = pfb.AnalysisPlan(taps, N, "8/7", var, 1, 0)
+    n_pol = 2 if args.workload == "c4" else 1
+    x = (torch.complex(torch.randn((n_pol, n), device=dev, generator=g),
+                       torch.randn((n_pol, n), device=dev, generator=g)) / np.sqrt(2)).to(torch.complex64)
+    ana = pfb.AnalysisPlan(taps, N, "8/7", var, n_pol, 0)
     win = pfb.PFBWindow().lookup["tukey"](nf, ov)
-    syn = pfb.SynthesisPlan(N, "8/7", nf, ov, True, 1, True, taps, win, None, 1, 0)
+    syn = pfb.SynthesisPlan(N, "8/7", nf, ov, True, 1, True, taps, win, None, n_pol, 0)
     if args.workload == "c2syn":
         chan = ana.execute(x).contiguous()
         torch.cuda.synchronize()
@@ -39,8 +41,8 @@ def main():
             syn.execute(chan, layout="ptc")
     else:
         K = ana.output_length(n)
-        chan = torch.empty((1, K, N), dtype=torch.complex64, device=dev)
-        out = torch.empty((1, syn.output_length(K)), dtype=torch.complex64, device=dev)
+        chan = torch.empty((n_pol, K, N), dtype=torch.complex64, device=dev)
+        out = torch.empty((n_pol, syn.output_length(K)), dtype=torch.complex64, device=dev)
         for _ in range(args.steps):
             pfb.roundtrip(ana, syn, x, chan=chan, out=out)
     torch.cuda.synchronize()
