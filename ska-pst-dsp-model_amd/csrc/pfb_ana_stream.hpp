@@ -69,6 +69,14 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
   constexpr int M = SH::M, PE = SH::PE, QS = SH::QS, T = SH::T, NEW = SH::NEW, WIN = SH::WIN;
   extern __shared__ __attribute__((aligned(16))) float2 smem[];
   const int c = threadIdx.x;
+  if (a.carry_out) {
+    // the next call's carry, grid-stride over this polarisation's workgroups (its few
+    // thousand samples are a fraction of one row of work per workgroup); before any early
+    // return, so every workgroup takes its share
+    const float2* src = a.in + pol * a.in_pol_stride + a.carry_src;
+    float2* dst = a.carry_out + pol * a.carry_pol_stride;
+    for (int64_t i = (int64_t)w * NT + c; i < a.carry_n; i += (int64_t)nw * NT) dst[i] = src[i];
+  }
   // this workgroup's steps (XCD-aware order: neighbouring ranges share halo rows in L2)
   const int64_t q_lo = a.row0 / NU;
   const int64_t n_steps = ((a.K + NU - 1) / NU - q_lo + QS - 1) / QS;

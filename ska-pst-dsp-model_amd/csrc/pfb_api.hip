@@ -228,6 +228,7 @@ struct pfb_analysis_plan {
   DevBuf zrev;  // padded generic round trip: index reversal (N - i) mod N of the row FFT input
   // streaming (FilterBank.m:13-14 input_buffer / buffered_samples)
   DevBuf carry, work, stage_in, stage_out;
+  DevBuf carry_next;  // device streams: the streaming kernel writes the next carry here, then swap
   int64_t buffered = 0;
   // round trip (pfb_roundtrip_execute): the analysis runs on this stream, ahead of the
   // synthesis on the caller's stream; one event per chunk orders them
@@ -251,12 +252,18 @@ static pfb::AnalysisArgs analysis_args(const pfb_analysis_plan* p, const float2*
                                        int64_t K_total, float2* z, int64_t z_ps, int64_t z_row0, int64_t pad,
                                        const OutLayout* lay, int zblk, const float2* pre = nullptr);
 
+// the next call's carry copied by the streaming kernel itself (AnalysisArgs::carry_out)
+struct CarryOut {
+  float2* dst;
+  int64_t src, n, dst_ps;
+};
+
 static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t in_ps, int64_t n_dat,
                                float2* out, int64_t out_ps, int64_t row0, int64_t K_end,
                                int64_t K_total, hipStream_t s, float2* z = nullptr,
                                int64_t z_ps = 0, int64_t z_row0 = 0, int64_t pad = 0,
                                const OutLayout* lay = nullptr, int zblk = 0, const float2* pre = nullptr,
-                               int z_stage = 0) {
+                               int z_stage = 0, const CarryOut* co = nullptr) {
   if (K_end <= row0) return PFB_OK;
   if (p->variant == pfb::kLowCbf) {
     pfb::LowCbfArgs l{};
@@ -278,6 +285,12 @@ static pfb_status analysis_run(pfb_analysis_plan* p, const float2* in, int64_t i
   pfb::AnalysisArgs a = analysis_args(p, in, in_ps, n_dat, out, out_ps, row0, K_end, K_total, z, z_ps, z_row0,
                                       pad, lay, zblk, pre);
   a.z_stage = z_stage;
+  if (co) {
+    a.carry_out = co->dst;
+    a.carry_src = co->src;
+    a.carry_n = co->n;
+    a.carry_pol_stride = co->dst_ps;
+  }
   a.scratch = nullptr;
   if (!p->fused && !z) {
     HIPCHK(p->scratch.ensure((size_t)p->n_pol * (K_end - row0) * p->N * sizeof(float2)));
@@ -477,7 +490,7 @@ static void analysis_host_tables(const pfb_analysis_desc* d, const pfb_analysis_
 }
 
 static void analysis_release(pfb_analysis_plan* p) {
-  for (DevBuf* b : {&p->taps, &p->twN, &p->zrev, &p->gtab, &p->scratch, &p->carry, &p->work, &p->stage_in,
+  for (DevBuf* b : {&p->taps, &p->twN, &p->zrev, &p->gtab, &p->scratch, &p->carry, &p->carry_next, &p->work, &p->stage_in,
                     &p->stage_out})
     b->release();
 }
@@ -656,15 +669,18 @@ static pfb_status filterbank_exec(pfb_analysis_plan* p, const pfb_cf32* in, int6
         // before it; then the new carry (stream order: after the kernel read the old one).
         // (Round 5: the bound was P N; a cascade's stage-2 carry of up to P N + NU M samples
         // per series then took the stitched path — two copies and a small launch per call.)
-        pfb_status st = analysis_run(p, (const float2*)in, in_ps, n_in, (float2*)out, out_ps, 0, Kt, K, s,
-                                     nullptr, 0, 0, B, lay, 0, p->carry.as<float2>());
-        if (st != PFB_OK) return st;
+        // (round 5) the kernel also copies the next carry into the second carry buffer —
+        // no copy launch after it — and the two buffers swap
         const int64_t nb = total - input_idat;
+        CarryOut co{nullptr, input_idat - B, nb, nb};
         if (nb > 0) {
-          HIPCHK(p->carry.ensure((size_t)p->n_pol * nb * sizeof(float2)));
-          HIPCHK(copy_pols(p->carry.as<float2>(), nb, (const float2*)in + (input_idat - B), in_ps, nb,
-                           p->n_pol, hipMemcpyDeviceToDevice, s));
+          HIPCHK(p->carry_next.ensure((size_t)p->n_pol * nb * sizeof(float2)));
+          co.dst = p->carry_next.as<float2>();
         }
+        pfb_status st = analysis_run(p, (const float2*)in, in_ps, n_in, (float2*)out, out_ps, 0, Kt, K, s,
+                                     nullptr, 0, 0, B, lay, 0, p->carry.as<float2>(), 0, nb > 0 ? &co : nullptr);
+        if (st != PFB_OK) return st;
+        if (nb > 0) std::swap(p->carry, p->carry_next);
         p->buffered = std::max<int64_t>(nb, 0);
         return PFB_OK;
       }

@@ -63,7 +63,8 @@ struct AnalysisArgs {
   int64_t pad;
   // with pad > 0: the pad samples in front of `in` are pre[pol][0, pad) (a stream object's
   // carried samples; null: zeros, the LowCBF pre-padding).  Streaming kernel only, read by the
-  // first workgroup's first window (launch_stream rejects pad > WIN N; the caller keeps B <= P N)
+  // first window of every workgroup whose window starts before `in` (launch_stream rejects
+  // pad > WIN N)
   const float2* pre;
   int64_t pre_pol_stride;
   float lcbf_scale;  // LowCBF streaming path: output scale (2^12)
@@ -82,6 +83,11 @@ struct AnalysisArgs {
   // row FFT (channelised rows from Z) — so the row FFT can run beside the synthesis, which
   // reads the same Z rows
   int z_stage;
+  // stream objects (streaming kernel only): also copy in[pol][carry_src, carry_src + carry_n)
+  // — the next call's carry, FilterBank.m:119-126 — to carry_out[pol][0, carry_n) (a buffer
+  // other than `pre`), spread over the grid before the main loop: no separate copy launch
+  float2* carry_out;
+  int64_t carry_src, carry_n, carry_pol_stride;
 };
 // SKA-Low CBF PST filterbank through the streaming analysis kernel (pfb_analysis.hip)
 hipError_t launch_lowcbf_stream(const AnalysisArgs& a, hipStream_t s);
