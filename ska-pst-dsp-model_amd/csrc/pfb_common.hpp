@@ -229,6 +229,7 @@ struct RowStore {
   float scale;
   int64_t row_base, n_total;  // output row = row_base + r (circularly shifted by -sds mod n_total)
   int zs;  // rows in runs of 2^zs per column (the wave synthesis' stage-1 row layout); 0: [row][c]
+  int nt;  // nontemporal stores (PFB_NT_ROW) — 0: default policy, for rows read right after
   __device__ __forceinline__ void store(int row, int c, float2 v) const {
     const int64_t r = r0 + row;
     if (r < n_rows) {
@@ -238,7 +239,8 @@ struct RowStore {
         while (t < 0) t += n_total;
       }
       const int64_t i = zs ? ((((t >> zs) * N + c) << zs) + (t & ((1 << zs) - 1))) : t * N + c;
-      st_nt<kNtRow>(out + i, cscale(v, scale));
+      if (nt) st_nt<kNtRow>(out + i, cscale(v, scale));
+      else out[i] = cscale(v, scale);
     }
   }
 };
@@ -267,6 +269,7 @@ struct RowFftArgs {
   int64_t row_base;  // global index of row 0 (output row = row_base + r, then the remap)
   int64_t n_total;   // rows of the whole call (remap modulus)
   int zs = 0;        // output rows in runs of 2^zs per column (RowStore::zs)
+  int nt = 1;        // RowStore::nt (the 4096-point kernel's rows are always nontemporal)
 };
 
 template <int N>
@@ -283,7 +286,7 @@ __global__ __launch_bounds__(NT) void row_fft_kernel(RowFftArgs a) {
   const int64_t r0 = (int64_t)blockIdx.x * ROWS;
   RowLoad<PERM, GAIN> ld{a.in + pol * a.in_pol_stride, r0, a.n_rows - 1, N, a.perm, a.cgain};
   RowStore st{a.out + pol * a.out_pol_stride, r0, a.n_rows, N, a.sds, a.remap, a.scale,
-              a.row_base, a.n_total, a.zs};
+              a.row_base, a.n_total, a.zs, a.nt};
   LdsRows rows(smem, RowShape<N>::RS);
   // twiddle table -> LDS behind the rows (ordered before pass 2 by its barrier)
   float2* tw = smem + ROWS * RowShape<N>::RS;
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
     for (int r = 0; r < R; ++r) rows.store(0, tid * R + r, v[r]);
     __syncthreads();
     RowStore st{a.out + pol * a.out_pol_stride, row, a.n_rows, N, a.sds, a.remap, a.scale,
-                a.row_base, a.n_total, a.zs};
+                a.row_base, a.n_total, a.zs, a.nt};
     run_rest<N, DIR>(rows, st, (const float2*)tw, tid, typename FFTPlan<N>::type{});
   }
 }

@@ -249,8 +249,16 @@ bool chan_ifft_supported(int N) { return pow2_supported(N) || mixed_chan_support
 
 hipError_t launch_chan_ifft(const ChanIfftArgs& c, hipStream_t s) {
   if (c.n_rows <= 0) return hipSuccess;
+  // (the stage-1 rows are read by the synthesis right after: default store policy while they
+  // fit the 256 MB Infinity Cache with room to spare — the nontemporal rows of the generic
+  // policy made the synthesis-only C2 path's block kernel read them from HBM)
+  bool fits = (double)c.n_pol * c.n_rows * c.N * 8.0 <= 160.0 * (1 << 20);
+  if constexpr (kExperiments) {  // (PFB_CHAN_IFFT_NT=1: nontemporal as before, A/B)
+    static const bool force_nt = knob("PFB_CHAN_IFFT_NT") && std::atoi(knob("PFB_CHAN_IFFT_NT")) == 1;
+    if (force_nt) fits = false;
+  }
   RowFftArgs r{c.in, c.in_pol_stride, c.out, c.out_pol_stride, c.n_rows, c.perm, c.cgain, c.twN,
-               1.0f, 0, 0, 0, c.n_rows, c.zblk == 4 ? 2 : c.zblk == 2 ? 1 : 0};
+               1.0f, 0, 0, 0, c.n_rows, c.zblk == 4 ? 2 : c.zblk == 2 ? 1 : 0, fits ? 0 : 1};
   if (c.zblk != 1 && c.zblk != 2 && c.zblk != 4) return hipErrorInvalidValue;
   return dispatch_row_fft<+1>(c.N, r, c.n_pol, s);
 }
