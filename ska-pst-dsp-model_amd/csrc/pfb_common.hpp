@@ -213,7 +213,7 @@ struct RowLoad {
   __device__ __forceinline__ float2 load(int row, int i) const {
     const int64_t r = min(r0 + row, last);
     const int c = PERM ? perm[i] : i;
-    float2 v = in[r * N + c];
+    float2 v = ld_nt<kNtlRow>(in + r * N + c);
     if constexpr (GAIN) v = cscale(v, cgain[c]);  // taper acts on input rows (before re-ordering)
     return v;
   }
