@@ -248,8 +248,9 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
   // inverse DFT across channels of row t = the row FFT of these sums, i.e. N^2 times
   // this row (Bunton: same column; padded, whose row FFT is an inverse one: column
   // (-pos) mod N), at the padded variant's circularly shifted row t = (k - sds) mod K
-  float2* zc = a.z ? a.z + pol * a.z_pol_stride + (VARIANT == kBunton ? pos : (N - pos) % N)
-                   : nullptr;
+  const int zcol = VARIANT == kBunton ? pos : (N - pos) % N;
+  float2* zc = a.z ? a.z + pol * a.z_pol_stride : nullptr;
+  const bool zrun = a.zblk == 2;  // Z rows in 2-row runs per column (the SKA-Mid wave synthesis)
   const float zscale = (float)N * (float)N;
   auto emit = [&](int64_t k, v2f acc) {
     if (!zc) sc[(k - a.row0) * N] = make_float2(acc.x, acc.y);
@@ -259,7 +260,8 @@ __global__ __launch_bounds__(NT) void fir_window_kernel(AnalysisArgs a, int rang
         t = k - a.sds;
         while (t < 0) t += a.K_total;
       }
-      if (t >= a.z_row0) st_nt<kNtFirZ>(zc + (t - a.z_row0) * N, make_float2(zscale * acc.x, zscale * acc.y));
+      if (t >= a.z_row0)
+        st_nt<kNtFirZ>(zc + z_index(t - a.z_row0, zcol, N, zrun), make_float2(zscale * acc.x, zscale * acc.y));
     }
   };
   if constexpr (U > 1) {
@@ -461,7 +463,8 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges,
   const int pos = VARIANT == kBunton ? c : N - 1 - c;
   float2* sc = a.scratch + (int64_t)pol * (a.K - a.row0) * N + pos;
   const int zcol = VARIANT == kBunton ? pos : (N - pos) % N;
-  float2* zc = a.z ? a.z + pol * a.z_pol_stride + zcol : nullptr;
+  float2* zc = a.z ? a.z + pol * a.z_pol_stride : nullptr;
+  const bool zrun = a.zblk == 2;  // Z rows in 2-row runs per column (the SKA-Mid wave synthesis)
   const float zscale = (float)N * (float)N;
   auto emit = [&](int64_t k, v2f acc) {
     if (k < a.row0 || k >= a.K) return;
@@ -473,7 +476,8 @@ __global__ __launch_bounds__(NT) void fir_lds_kernel(AnalysisArgs a, int ranges,
         t = k - a.sds;
         while (t < 0) t += a.K_total;  // once, unless the series is shorter than sds rows
       }
-      if (t >= a.z_row0) st_nt<kNtFirZ>(zc + (t - a.z_row0) * N, make_float2(zscale * acc.x, zscale * acc.y));
+      if (t >= a.z_row0)
+        st_nt<kNtFirZ>(zc + z_index(t - a.z_row0, zcol, N, zrun), make_float2(zscale * acc.x, zscale * acc.y));
     }
   };
 
@@ -743,11 +747,16 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
   if (a.K <= a.row0) return hipSuccess;
   if (a.pad != 0 && !analysis_takes_offset(a)) return hipErrorInvalidValue;
   if (a.z && !analysis_can_emit_z(a)) return hipErrorInvalidValue;
-  if (a.z && a.zblk > 1 &&
-      (!analysis_can_emit_zblk(a) || ((a.row0 - a.z_row0) % 16) != 0 || (a.zblk != 2 && a.zblk != 4)))
-    return hipErrorInvalidValue;
   bool fused = false;
   if (!analysis_supported(a.N, a.P, a.variant, &fused)) return hipErrorInvalidValue;
+  // stage-1 rows in runs: the streaming kernel's 2/4/16-row runs (N = 256), or the 2-row
+  // runs of the generic path's FIR (fir_lds / fir_window) for the SKA-Mid wave synthesis
+  if (a.z && a.zblk > 1) {
+    const bool stream_ok = analysis_can_emit_zblk(a) && ((a.row0 - a.z_row0) % 16) == 0 &&
+                           (a.zblk == 2 || a.zblk == 4);
+    const bool generic_ok = !fused && a.zblk == 2 && a.z_row0 == 0 && fir_window_applies(a);
+    if (!stream_ok && !generic_ok) return hipErrorInvalidValue;
+  }
   static const bool no_stream = knob("PFB_ANALYSIS_NO_STREAM") != nullptr;
   if (fused && stream_shape(a) && !no_stream) {
     static const int mask = knob("PFB_ANA_MASK") ? std::atoi(knob("PFB_ANA_MASK")) : 0;
@@ -789,8 +798,12 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
     // (z_stage 2 on rows [row0, K): Z rows are output rows, so both sides start at row0)
     if ((a.row0 != 0 && a.z_stage != 2) || a.z_row0 != 0 || (a.variant == kPadded && !a.zrev))
       return hipErrorInvalidValue;
+    // (2-row runs: row0 of the row FFT is even — the round trip runs it from row 0 — so the
+    // run of row0 starts at element row0 N)
+    if (a.zblk == 2 && (a.row0 & 1)) return hipErrorInvalidValue;
     RowFftArgs rz{a.z + a.row0 * a.N, a.z_pol_stride, a.out + a.row0 * a.N, a.out_pol_stride, rows, a.zrev,
                   nullptr, a.twN, 1.0f / (float)a.N, 0, 0, 0, a.K_total};
+    rz.in_run = a.zblk == 2 ? 1 : 0;
     if (a.variant == kBunton) return dispatch_row_fft<-1>(a.N, rz, a.n_pol, s);
     return dispatch_row_fft<+1>(a.N, rz, a.n_pol, s);
   }

@@ -202,6 +202,13 @@ struct LcbfRowStore {
 // Row loader of the first FFT pass.  Rows past the end are clamped to the last valid
 // row (their results are never stored), so every load is unconditional and the
 // compiler can issue them back to back.
+// Element (row, c) of a [row][N] array, or of its 2-row-run layout (run = true: rows 2g and
+// 2g + 1 of column c at [g][c][0 / 1], i.e. 128-B lines of 2 rows x 8 columns) — the stage-1
+// rows of the SKA-Mid round trip (FIR -> row FFT / synth_wave512_kernel)
+__host__ __device__ __forceinline__ int64_t z_index(int64_t row, int c, int N, bool run) {
+  return run ? (((row >> 1) * N + c) << 1) + (row & 1) : row * N + c;
+}
+
 template <bool PERM, bool GAIN>
 struct RowLoad {
   static constexpr bool kIsLds = false;
@@ -210,10 +217,11 @@ struct RowLoad {
   int N;
   const int* perm;
   const float* cgain;
+  int run;  // 2-row-run input layout (z_index)
   __device__ __forceinline__ float2 load(int row, int i) const {
     const int64_t r = min(r0 + row, last);
     const int c = PERM ? perm[i] : i;
-    float2 v = ld_nt<kNtlRow>(in + r * N + c);
+    float2 v = ld_nt<kNtlRow>(in + z_index(r, c, N, run));
     if constexpr (GAIN) v = cscale(v, cgain[c]);  // taper acts on input rows (before re-ordering)
     return v;
   }
@@ -270,6 +278,7 @@ struct RowFftArgs {
   int64_t n_total;   // rows of the whole call (remap modulus)
   int zs = 0;        // output rows in runs of 2^zs per column (RowStore::zs)
   int nt = 1;        // RowStore::nt (the 4096-point kernel's rows are always nontemporal)
+  int in_run = 0;    // input rows in 2-row runs per column (z_index), the SKA-Mid stage-1 rows
 };
 
 template <int N>
@@ -284,7 +293,7 @@ __global__ __launch_bounds__(NT) void row_fft_kernel(RowFftArgs a) {
   extern __shared__ __attribute__((aligned(16))) float2 smem[];
   const int pol = blockIdx.y;
   const int64_t r0 = (int64_t)blockIdx.x * ROWS;
-  RowLoad<PERM, GAIN> ld{a.in + pol * a.in_pol_stride, r0, a.n_rows - 1, N, a.perm, a.cgain};
+  RowLoad<PERM, GAIN> ld{a.in + pol * a.in_pol_stride, r0, a.n_rows - 1, N, a.perm, a.cgain, a.in_run};
   RowStore st{a.out + pol * a.out_pol_stride, r0, a.n_rows, N, a.sds, a.remap, a.scale,
               a.row_base, a.n_total, a.zs, a.nt};
   LdsRows rows(smem, RowShape<N>::RS);
@@ -349,7 +358,7 @@ __global__ __launch_bounds__(NT) void row_fft_persist_kernel(RowFftArgs a) {
   float2 pf[R];
   auto load_row = [&](int64_t row) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) pf[r] = ld_nt<kNtlRow>(in + row * N + col[r]);
+    for (int r = 0; r < R; ++r) pf[r] = ld_nt<kNtlRow>(in + z_index(row, col[r], N, a.in_run));
   };
   load_row(q0);
   vm_drain();

@@ -225,9 +225,13 @@ void synth_wave512_kernel(SynthBlockArgs a) {
   const char* tw2row = lds + kTw2Off + (2 * f1 + h) * kRow14B;
   const char* winrow = lds + kWinOff + m * kWinRowB;
 
-  const float2* zpol = a.Z + pol * a.z_pol_stride + t0g;
+  const float2* zpol = a.Z + pol * a.z_pol_stride + (a.zblk == 2 ? 2 * t0g : t0g);
   const uint32_t zbytes = (tmask(a.timing_mask) & 1) ? 0u : (uint32_t)((511 * N + kW5Cols) * 8);
-  const uint32_t zlane = (uint32_t)((m * N + c1) * 8);
+  // (zblk 2: Z rows in 2-row runs per column, z_index — lanes m and m + 1 read one 16-B pair,
+  // a load instruction 4 whole 128-B lines of 2 rows x 8 phases instead of 8 half lines; the
+  // row offsets 32 r N are pair-aligned, the same bytes either way)
+  const uint32_t zlane = a.zblk == 2 ? (uint32_t)(((((m >> 1) * N + c1) << 1) + (m & 1)) * 8)
+                                     : (uint32_t)((m * N + c1) * 8);
   float2* opol = a.out + pol * a.out_pol_stride;
 
   float2 x[16];  // raw Z values of the next block, rows m + 32 r
@@ -369,7 +373,7 @@ void synth_wave512_kernel(SynthBlockArgs a) {
 bool synth_wave512_supported(const SynthBlockArgs& a) {
   // (32-bit byte offsets: 512 rows x N phases x 8 B per block stay below 2^31)
   // (L_ov = 112 N: pass B forms and stores only t1b in [4, 12))
-  return a.Nf == 512 && a.W == 448 && a.keep == 256 && a.zblk <= 1 && a.N % kW5Cols == 0 &&
+  return a.Nf == 512 && a.W == 448 && a.keep == 256 && (a.zblk <= 2) && a.N % kW5Cols == 0 &&
          a.N <= 65536 && a.tw4s != nullptr && a.Lov == 112 * a.N;
 }
 
