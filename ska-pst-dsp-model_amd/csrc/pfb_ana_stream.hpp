@@ -69,13 +69,19 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
   constexpr int M = SH::M, PE = SH::PE, QS = SH::QS, T = SH::T, NEW = SH::NEW, WIN = SH::WIN;
   extern __shared__ __attribute__((aligned(16))) float2 smem[];
   const int c = threadIdx.x;
+  if constexpr (ZOUT == 0 && !LCBF) {  // (stream objects only: no round-trip / LowCBF kernel)
   if (a.carry_out) {
     // the next call's carry, grid-stride over this polarisation's workgroups (its few
     // thousand samples are a fraction of one row of work per workgroup); before any early
     // return, so every workgroup takes its share
+    // (a uniform loop with a per-lane guard — no lane-dependent trip count)
     const float2* src = a.in + pol * a.in_pol_stride + a.carry_src;
     float2* dst = a.carry_out + pol * a.carry_pol_stride;
-    for (int64_t i = (int64_t)w * NT + c; i < a.carry_n; i += (int64_t)nw * NT) dst[i] = src[i];
+    for (int64_t i0 = (int64_t)w * NT; i0 < a.carry_n; i0 += (int64_t)nw * NT) {
+      const int64_t i = i0 + c;
+      if (i < a.carry_n) dst[i] = src[i];
+    }
+  }
   }
   // this workgroup's steps (XCD-aware order: neighbouring ranges share halo rows in L2)
   const int64_t q_lo = a.row0 / NU;
@@ -221,7 +227,7 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
       const int hi = (int)min(max(a.K - k0, (int64_t)0), (int64_t)T);
       const int lo = (int)min(max(a.row0 - k0, (int64_t)0), (int64_t)T);
       const __amdgpu_buffer_rsrc_t r =
-          make_rsrc(opol + k0, hi > 0 ? (uint32_t)(((int64_t)(N - 1) * a.out_cs + hi) * 8) : 0u);
+          make_rsrc_u(opol + k0, hi > 0 ? (uint32_t)(((int64_t)(N - 1) * a.out_cs + hi) * 8) : 0u);
       static_for<0, (T / 2) * N / NT>([&](auto iv) {
         const int idx = c + decltype(iv)::value * NT;
         const int ch = idx / (T / 2), r0 = 2 * (idx % (T / 2));

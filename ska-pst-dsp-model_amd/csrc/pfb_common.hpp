@@ -140,7 +140,7 @@ struct BufRowStore {
                                                       int64_t k_hi, int N, float scale) {
     const int64_t hi = min(max(k_hi - k0, (int64_t)0), (int64_t)T);
     const int lo = (int)min(max(k_lo - k0, (int64_t)0), (int64_t)T);
-    return BufRowStore{make_rsrc(base + k0 * N, (uint32_t)(hi * N * 8)), lo, N, scale};
+    return BufRowStore{make_rsrc_u(base + k0 * N, (uint32_t)(hi * N * 8)), lo, N, scale};
   }
 };
 
@@ -156,11 +156,13 @@ struct StridedRowStore {
   int lo, hi, rs, cs, split, shift, nsel;
   float scale;
   __device__ __forceinline__ void store(int row, int c, float2 v) const {
+    // (bitwise, not short-circuit: the && chains compiled into divergent branches, two
+    // exec-mask round trips per store)
     int j = c;
-    bool ok = row >= lo && row < hi;
-    if (nsel > 0) {
+    bool ok = (row >= lo) & (row < hi);
+    if (nsel > 0) {  // uniform
       j = c < split ? c : c - shift;
-      ok = ok && (c < split || c >= split + shift) && j < nsel;
+      ok = ok & ((c < split) | (c >= split + shift)) & (j < nsel);
     }
     const uint32_t off = ok ? (uint32_t)((row * rs + j * cs) * 8) : 0xFFFFFFF0u;
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v, scale)), r, off, 0, kAuxStrided);
@@ -173,7 +175,7 @@ struct StridedRowStore {
     const int lo = (int)min(max(k_lo - k0, (int64_t)0), (int64_t)T);
     const int jn = nsel > 0 ? nsel : N;
     const uint32_t bytes = hi > 0 ? (uint32_t)(((int64_t)(hi - 1) * rs + (int64_t)(jn - 1) * cs + 1) * 8) : 0u;
-    return StridedRowStore{make_rsrc(base + k0 * rs, bytes), lo, hi, rs, cs, split, shift, nsel, scale};
+    return StridedRowStore{make_rsrc_u(base + k0 * rs, bytes), lo, hi, rs, cs, split, shift, nsel, scale};
   }
 };
 
@@ -195,7 +197,7 @@ struct LcbfRowStore {
                                                        int64_t k_hi, float scale) {
     const int64_t hi = min(max(k_hi - k0, (int64_t)0), (int64_t)T);
     const int lo = (int)min(max(k_lo - k0, (int64_t)0), (int64_t)T);
-    return LcbfRowStore{make_rsrc(base + k0 * 216, (uint32_t)(hi * 216 * 8)), lo, scale};
+    return LcbfRowStore{make_rsrc_u(base + k0 * 216, (uint32_t)(hi * 216 * 8)), lo, scale};
   }
 };
 

@@ -72,6 +72,17 @@ __device__ __forceinline__ v2u as_u(v2f x) { return __builtin_bit_cast(v2u, x); 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
+// The same from values that ARE wave-uniform but that the uniformity analysis may not prove
+// so (computed after divergent control flow, through loops): read from the first lane, so
+// the descriptor lives in scalar registers.  Otherwise every buffer access through it
+// becomes a one-trip waterfall loop (measured: the strided-store cascade kernel had 33 of
+// them per step, the LowCBF kernel 17 after an unrelated divergent loop was added).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_u(const void* base, uint32_t bytes) {
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  const uint64_t bu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  return make_rsrc(reinterpret_cast<const void*>(bu), (uint32_t)__builtin_amdgcn_readfirstlane(bytes));
+}
 
 // s_waitcnt vmcnt(0) (gfx9 encoding: expcnt / lgkmcnt left at their maxima).  A software-
 // pipelined loop whose prologue issues the first loads should drain them before the loop:
