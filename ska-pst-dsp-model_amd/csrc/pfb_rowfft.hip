@@ -83,7 +83,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void ro
   // input in 2-row runs (a.in_run, z_index): element e of row rr at ((rr / 2) N + e) 2 + rr % 2
   // — the lane and register strides double; the pair's other row is fetched with the same
   // 128-B lines one row later (L2 / Infinity-Cache hits)
-  const int ish = a.in_run ? 1 : 0;
+  const int ish = __builtin_amdgcn_readfirstlane(a.in_run ? 1 : 0);  // (scalar: the soffsets use it)
   const uint32_t lane_in = lane_off << ish;
   [[maybe_unused]] uint32_t col_in[PERM ? 16 : 1];
   if constexpr (PERM) {
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void ro
   float2 pf[16];
   auto load_row = [&](int64_t rr) {
     const int64_t base = a.in_run ? (((rr >> 1) * N) << 1) + (rr & 1) : rr * N;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(in + base, (uint32_t)((N * 8) << ish));
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc_u(in + base, (uint32_t)((N * 8) << ish));
     static_for<0, 16>([&](auto rv) {
       constexpr int r = decltype(rv)::value;
       const v2u x = PERM ? __builtin_amdgcn_raw_buffer_load_b64(rs, col_in[PERM ? r : 0], 0, kNtlRow ? 2 : 0)
