@@ -19,3 +19,7 @@ if [ -n "${PROF:-}" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o bench -- \
       python bench.py --steps 20 --warmup 3 > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || exit $?
 fi
+if [ -n "${C3K:-}" ]; then
+  ROUNDS=2 timeout -k 10 900 bash scripts/gpu_c3_kernel_ab.sh $C3K > gpurun_out/c3k.log 2>&1 || exit $?
+  cat gpurun_out/c3k.log
+fi
