@@ -1598,13 +1598,12 @@ static pfb_status roundtrip_run(pfb_analysis_plan* pa, pfb_synthesis_plan* ps, c
   static const int zb_knob = pfb::knob("PFB_ZBLK") ? std::atoi(pfb::knob("PFB_ZBLK")) : 2;
   int zblk = (!no_wave && analysis_emits_zblk(pa) && z0 == off && off % 16 == 0) ? zb_knob : 0;
   if (zblk && !pfb::synth_wave_supported(synth_args(ps, nullptr, 0, 0, B, nullptr, 0, 0, zblk))) zblk = 0;
-  // generic path (N > 256, the SKA-Mid round trip), experiments build (PFB_C3_ZRUN=1): the
-  // FIR writes the rows in 2-row runs per column, so the Nf = 512 wave synthesis loads whole
-  // 128-B lines (2 rows x 8 phases) — bit-identical; measured (profiles/r05_v16_*) the
-  // synthesis 16 us faster but the row FFT 13 us and the FIR 8 us slower (each row FFT row
-  // then fetches its pair's lines twice), so rows stay the default
-  static const bool zrun_on =
-      pfb::kExperiments && pfb::knob("PFB_C3_ZRUN") && std::atoi(pfb::knob("PFB_C3_ZRUN")) == 1;
+  // generic path (N > 256, the SKA-Mid round trip): the FIR writes the rows in 2-row runs
+  // per column, so the Nf = 512 wave synthesis loads whole 128-B lines (2 rows x 8 phases)
+  // — bit-identical; measured (profiles/r05_v17_c3_zrun_kernel_ab/) synthesis -17 us, FIR
+  // +8 us, row FFT +4 us (it reads each row's pair partner from the lines fetched one row
+  // earlier): net -5 us per unit (PFB_C3_ZRUN=0: rows, experiments build)
+  static const bool zrun_on = !(pfb::knob("PFB_C3_ZRUN") && std::atoi(pfb::knob("PFB_C3_ZRUN")) == 0);
   const bool zrun = zrun_on && !zblk && !pa->fused && analysis_emits_z(pa) && off % 2 == 0 &&
                     pfb::synth_wave512_supported(synth_args(ps, nullptr, 0, 0, B, nullptr, 0, 0, 2));
   if (zrun) zblk = 2;
