@@ -21,11 +21,14 @@ namespace pfb {
 // passes.  The tables take 8.7 KB instead of 32 KB of LDS: 3 workgroups per CU.
 // The row takes two layouts instead of the 1-in-16 pad (whose pass-2 / pass-3 loads wrapped
 // one lane of every 32-lane ds_read_b64 group onto bank 0: 2-way, 22 % of the LDS cycles,
-// r05_v4 PMC): pass 1 -> pass 2, element 16 j + r at slot 258 r + j (rows of 258 slots: the
-// 16-lane store groups and the 32-lane load groups, 258 (tid mod 16) + tid / 16, on distinct
+// r05_v4 PMC): pass 1 -> pass 2, element 16 j + r at slot kR4kA r + j (rows of kR4kA slots: the
+// 16-lane store groups and the load groups, kR4kA (tid mod 16) + tid / 16, on distinct
 // banks); pass 2 -> pass 3 unpadded (element e at slot e).  Every access is one lane base
 // plus an immediate offset.
-constexpr int kR4kA = 258;         // layout-A row of 16 j + r: slot kR4kA r + j (258 = 2 mod 32)
+// (257: the pass-2 loads compile to ds_read2_b64 — 16-lane groups on 32 banks — whose
+// 16 lanes k2 then sit at dword 2 (257 k2 + j) = 2 k2 + 2 j mod 32, all distinct; 258 gave
+// 4 k2 mod 32, 2-way, the 18 % of LDS cycles PMC kept counting)
+constexpr int kR4kA = 257;         // layout-A row of 16 j + r: slot kR4kA r + j
 constexpr int kR4kRow = 15 * kR4kA + 256 + 2;  // slots of the row buffer (layout A; B needs 4096)
 constexpr int kR4kTw2 = 4 * 16;    // T2[p][k] = tw[(2^p 16 k) mod N], k < 16
 constexpr int kR4kTw3 = 4 * 256;   // T3[p][k] = tw[2^p k], k < 256
