@@ -584,18 +584,18 @@ static hipError_t launch_fir_window_t(const AnalysisArgs& a, hipStream_t s) {
     ranges = (int)need;
   }
   dim3 grid((unsigned)(chunks * a.nu * ranges), (unsigned)a.n_pol);
-  auto go = [&](auto u) {
+  // (launch_kernel already read and cleared the launch error: return its value, a second
+  // hipGetLastError() would report a failed launch as hipSuccess)
+  auto go = [&](auto u) -> hipError_t {
     // (wide DE: the U DE loads in flight would not fit the register budget)
     constexpr int U = DE * decltype(u)::value <= 21 ? decltype(u)::value : 1;
     if (a.variant == kBunton)
-      (void)launch_kernel(fir_window_kernel<PW, DE, kBunton, U>, grid, dim3(NT), 0, s, a, ranges, slice_map);
-    else
-      (void)launch_kernel(fir_window_kernel<PW, DE, kPadded, U>, grid, dim3(NT), 0, s, a, ranges, slice_map);
+      return launch_kernel(fir_window_kernel<PW, DE, kBunton, U>, grid, dim3(NT), 0, s, a, ranges, slice_map);
+    return launch_kernel(fir_window_kernel<PW, DE, kPadded, U>, grid, dim3(NT), 0, s, a, ranges, slice_map);
   };
-  if (rows == 1) go(std::integral_constant<int, 1>{});
-  else if (rows == 2) go(std::integral_constant<int, 2>{});
-  else go(std::integral_constant<int, 3>{});
-  return hipGetLastError();
+  if (rows == 1) return go(std::integral_constant<int, 1>{});
+  if (rows == 2) return go(std::integral_constant<int, 2>{});
+  return go(std::integral_constant<int, 3>{});
 }
 
 // register-window FIR if the shape has an instance (window PW >= P, DE | exact M)

@@ -865,6 +865,7 @@ static pfb::SynthBlockArgs synth_args(const pfb_synthesis_plan* p, const float2*
 static pfb_status synthesis_spectral(pfb_synthesis_plan* p, const float2* in, int64_t in_ps, int64_t b0,
                                      int64_t nb, float2* out, int64_t out_ps, int64_t out_limit,
                                      hipStream_t s) {
+  p->last_stage1 = PFB_STAGE1_STORED;  // (the spectral passes read the channelised rows)
   const int64_t per_block = (int64_t)p->N * std::max(p->Nf, p->W);
   const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(65535, ((int64_t)1 << 26) / per_block));
   const int64_t nsub = std::min(sub, nb);

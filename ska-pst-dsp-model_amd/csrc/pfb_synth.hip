@@ -236,9 +236,8 @@ bool synth_block_supported(int Nf, int W) {
 hipError_t launch_synth_block(const SynthBlockArgs& a, hipStream_t s) {
   if (a.n_blocks <= 0) return hipSuccess;
   // SKA-Mid shape (Nf 512, W 448, Ov 128): the wave kernel, on rows or 2-row runs (zblk 2)
-  // (PFB_SYNTH_WAVE512=0: the block kernel, experiments build)
-  static const bool no_w5 = knob("PFB_SYNTH_WAVE512") && std::atoi(knob("PFB_SYNTH_WAVE512")) == 0;
-  if (!no_w5 && a.Nf == 512 && synth_wave512_supported(a)) return launch_synth_wave512(a, s);
+  // (PFB_SYNTH_WAVE512=0: the block kernel, experiments build — synth_wave512_supported)
+  if (a.Nf == 512 && synth_wave512_supported(a)) return launch_synth_wave512(a, s);
   // stage-1 rows for the Nf = 256 wave kernel (the fused round trip: zblk = run length)
   if (a.zblk || a.fir_x) return launch_synth_wave(a, s);
 #define X(a_, b_) \

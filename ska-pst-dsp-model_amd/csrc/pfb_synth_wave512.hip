@@ -39,6 +39,8 @@
 // (round 4: 37.6 % of the LDS cycles were bank conflicts, the model gives the same figure).
 #include "pfb_common.hpp"
 
+#include <cstdlib>
+
 namespace pfb {
 
 namespace {
@@ -371,6 +373,10 @@ void synth_wave512_kernel(SynthBlockArgs a) {
 }
 
 bool synth_wave512_supported(const SynthBlockArgs& a) {
+  // (PFB_SYNTH_WAVE512=0: the block kernel, experiments build — checked here so the round
+  // trip's 2-row Z layout, which only this kernel reads, is turned off with it)
+  static const bool no_w5 = knob("PFB_SYNTH_WAVE512") && std::atoi(knob("PFB_SYNTH_WAVE512")) == 0;
+  if (no_w5) return false;
   // (32-bit byte offsets: 512 rows x N phases x 8 B per block stay below 2^31)
   // (L_ov = 112 N: pass B forms and stores only t1b in [4, 12))
   return a.Nf == 512 && a.W == 448 && a.keep == 256 && (a.zblk <= 2) && a.N % kW5Cols == 0 &&

@@ -490,6 +490,11 @@ def roundtrip_synthesis(analysis: AnalysisPlan, synthesis: SynthesisPlan, n_dat:
         # only after the work just enqueued on this stream has finished
         if not t.cuda.is_current_stream_capturing():
             xin.record_stream(t.cuda.current_stream(out.device))
+        else:
+            # a captured launch holds the input's address for every replay: keep the tensor
+            # alive as long as the plan (one entry per address, so recaptures do not grow it)
+            held = synthesis.__dict__.setdefault("_graph_inputs", {})
+            held[xin.data_ptr()] = xin
         synthesis._rt_input = None
     return out
 

@@ -281,6 +281,62 @@ def test_two_stage_strided_matches_oracle(gpu):
         assert_pfb_close(got, ref, what=f"two-stage 256x256 strided n={n}")
 
 
+def _padded_cfg(taps, N, os_="8/7"):
+    return dict(analysis_function="polyphase_analysis_padded", filt_coeff=taps, channels=N,
+                os_factor=os_)
+
+
+@pytest.mark.parametrize("critical,single", [(0, 0), (1, 0), (0, 1)])
+def test_two_stage_padded_matches_oracle(gpu, critical, single):
+    """TwoStageFilterBank whose stages are both polyphase_analysis_padded (BASELINE
+    configs[2]: the `mid` sub-config names it, test.config.json:104-128, and
+    TwoStageFilterBank.m:27,51-52 builds every stage as FilterBank(config)) at reduced
+    channel counts (64 x 16), two calls, against TwoStageFilterBankOracle's nch1
+    separate padded FilterBank objects (TwoStageFilterBank.m:92-110).  Each padded call
+    restarts its commutator (the reference's behaviour); stage 2 is one
+    batched plan over the 64 stage-1 channels."""
+    pfb = _pfb()
+    taps1 = pfb.design_PFB_FIR_filter(64, "8/7", 12)
+    taps2 = pfb.design_PFB_FIR_filter(16, "8/7", 10)
+    ts = pfb.TwoStageFilterBank(_padded_cfg(taps1, 64)).set_stage2_config(_padded_cfg(taps2, 16))
+    ts.critical, ts.single = critical, single
+    ots = orc.TwoStageFilterBankOracle(
+        orc.FilterBankOracle(taps1, 64, "8/7", "polyphase_analysis_padded"),
+        lambda: orc.FilterBankOracle(taps2, 16, "8/7", "polyphase_analysis_padded"),
+        critical=bool(critical), single=bool(single))
+    rng = np.random.default_rng(23)
+    for n in (300_000, 123_457):
+        x = _noise(rng, (2, 1, n))
+        ts, got = ts.execute(x)
+        ref = ots.execute(x)
+        assert got.shape == ref.shape and got.shape[2] > 0, (got.shape, ref.shape)
+        assert_pfb_close(got, ref, what=f"padded two-stage 64x16 n={n}")
+
+
+def test_two_stage_padded_mid_stage1(gpu):
+    """The SKA-Mid stage 1 exactly (4096 ch, 8/7, the 100 353-tap two-stage design,
+    polyphase_analysis_padded) cascaded into a small padded stage 2 (16 ch) over all
+    4096 coarse channels, critical (TwoStageFilterBank.m:81-85,102-105), two calls,
+    against TwoStageFilterBankOracle."""
+    pfb = _pfb()
+    taps1 = pfb.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
+    assert len(taps1) == 100353
+    taps2 = pfb.design_PFB_FIR_filter(16, "8/7", 10)
+    ts = pfb.TwoStageFilterBank(_padded_cfg(taps1, 4096)).set_stage2_config(_padded_cfg(taps2, 16))
+    ts.critical = 1
+    ots = orc.TwoStageFilterBankOracle(
+        orc.FilterBankOracle(taps1, 4096, "8/7", "polyphase_analysis_padded"),
+        lambda: orc.FilterBankOracle(taps2, 16, "8/7", "polyphase_analysis_padded"),
+        critical=True, single=False)
+    rng = np.random.default_rng(24)
+    for n in (1_500_000, 1_000_003):
+        x = _noise(rng, (1, 1, n))
+        ts, got = ts.execute(x)
+        ref = ots.execute(x)
+        assert got.shape == ref.shape and got.shape[1] == 4096 * 14 and got.shape[2] > 0
+        assert_pfb_close(got, ref, what=f"padded two-stage 4096x16 n={n}")
+
+
 @pytest.mark.parametrize("critical,combine", [(False, 1), (True, 1), (True, 2)])
 def test_two_stage_inverse_matches_oracle(gpu, critical, combine):
     pfb = _pfb()

@@ -639,6 +639,43 @@ def test_synthesis_spectral_custom_and_combine(gpu):
                                 None, w.lookup["tukey"](128, 16))
 
 
+@pytest.mark.parametrize("so,chunks", [(5, (500, 333, 1000)), (200, (150, 700, 2100))])
+@pytest.mark.parametrize("device", [False, True])
+def test_inverse_filterbank_sample_offset_spectral_taper(gpu, so, chunks, device):
+    """sample_offset != 0 together with frequency_taper('hann') (InverseFilterBank.m:48-61,
+    92-96): the spectral-taper path takes the offset as a negative row shift into the
+    concatenated carry + input (pfb_api.hip synthesis_chunk) — against
+    InverseFilterBankOracle over several chunks, host and device input."""
+    import torch
+    pfb = _pfb()
+    taps = _taps("test")
+    cfg = dict(filt_coeff=taps, channels=8, os_factor="8/7", input_fft_length=128,
+               input_overlap=16, deripple=False, temporal_taper="tukey")
+    ifb = pfb.InverseFilterBank(cfg).frequency_taper("hann")
+    ifb.sample_offset = so
+    oifb = orc.InverseFilterBankOracle(taps, 8, "8/7", 128, 16, "tukey",
+                                       sample_offset=so).frequency_taper("hann")
+    rng = np.random.default_rng(57 + so)
+    produced = 0
+    for n in chunks:
+        x = _noise(rng, (2, 8, n))
+        xin = torch.from_numpy(x).to(gpu) if device else x
+        try:
+            ref = oifb.execute(x)
+        except ValueError:
+            with pytest.raises(pfb.PfbError):
+                ifb.execute(xin)
+            continue
+        ifb, got = ifb.execute(xin)
+        got = got.cpu().numpy() if hasattr(got, "cpu") else np.asarray(got)
+        assert got.shape == ref.shape, (n, got.shape, ref.shape)
+        if ref.size:
+            assert_pfb_close(got, ref, what=f"inverse hann offset {so} chunk {n}")
+        produced += ref.shape[2]
+        assert ifb.buffered_samples == oifb.buffered_samples
+    assert produced > 0
+
+
 def test_inverse_filterbank_frequency_taper_stream(gpu):
     """InverseFilterBank.frequency_taper('hann') (InverseFilterBank.m:48-61) streaming."""
     pfb = _pfb()

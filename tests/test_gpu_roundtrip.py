@@ -364,6 +364,53 @@ def test_c2_full_size_matches_oracle(c2):
     assert_pfb_close(c2["out"][:, None, :], ref, scale=1.0, what="C2 round trip (raw)")
 
 
+def test_c2_full_size_standalone_synthesis(c2):
+    """The synthesis alone on the WHOLE C2 channelised product (74 883 rows, 467 blocks)
+    — ``SynthesisPlan.execute(chan)``, the path bench.py's ``synthesis_only`` times (the
+    PST production case: InverseFilterBank.m:92-96 -> polyphase_synthesis.m:163-316; row
+    FFT stage 1 + synth_wave_kernel) — against the oracle synthesis of the same
+    channelised product, every output sample (16 737 280) at the raw 1e-6 criterion."""
+    import torch
+    pfb = _pfb()
+    taps, chan = c2["taps"], c2["chan"]                       # (1, K, 256) from the GPU
+    win = pfb.PFBWindow().lookup["tukey"](256, 48)
+    syn = pfb.SynthesisPlan(256, "8/7", 256, 48, True, 1, True, taps, win, None, 1, 0)
+    out = syn.execute(torch.from_numpy(chan).to(c2["xd"].device), 1, layout="ptc")
+    torch.cuda.synchronize()
+    assert syn.last_stage1_rows == "stored"
+    ref = orc.polyphase_synthesis(chan.transpose(0, 2, 1), 1, 256, "8/7",
+                                  {"apply_deripple": 1, "filter_coeff": taps}, 1, 48,
+                                  orc.pfb_window("tukey", 256, 48))
+    assert out.shape == (1, 16737280)
+    assert_pfb_close(out.cpu().numpy()[:, None, :], ref, scale=1.0, what="C2 synthesis only (raw)")
+    syn.close()
+
+
+def test_c2_full_size_inverse_filterbank_stream(c2):
+    """InverseFilterBank streaming over the whole C2 channelised product in three device
+    chunks (InverseFilterBank.m:73-135: carry-over rounded up to a multiple of nu,
+    deripple forced off at :90) against InverseFilterBankOracle on the same chunks."""
+    import torch
+    pfb = _pfb()
+    taps, chan = c2["taps"], c2["chan"]
+    cfg = dict(filt_coeff=taps, channels=256, os_factor="8/7", input_fft_length=256,
+               input_overlap=48, deripple=True, temporal_taper="tukey")
+    ifb = pfb.InverseFilterBank(cfg)
+    oifb = orc.InverseFilterBankOracle(taps, 256, "8/7", 256, 48, "tukey", deripple=True)
+    cd = torch.from_numpy(chan).to(c2["xd"].device)
+    K = chan.shape[1]
+    cuts = [0, 30001, 55555, K]
+    total = 0
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        ifb, got = ifb.execute(cd[:, a:b, :].transpose(1, 2))   # (n_pol, n_chan, n) view
+        ref = oifb.execute(chan[:, a:b, :].transpose(0, 2, 1))
+        assert tuple(got.shape) == ref.shape, (a, b, tuple(got.shape), ref.shape)
+        assert_pfb_close(got.cpu().numpy(), ref, scale=1.0, what=f"C2 inverse stream rows [{a}, {b})")
+        assert ifb.buffered_samples == oifb.buffered_samples
+        total += ref.shape[2]
+    assert total > 16_000_000
+
+
 def test_c2_full_size_linearity(c2):
     """Size-independent property: RT(a x1 + b x2) = a RT(x1) + b RT(x2)."""
     import torch
