@@ -287,6 +287,14 @@ def pmc_traffic(path=PMC_TRAFFIC):
         return json.load(f)
 
 
+# why a kernel's measured HBM bytes exceed 1.6x its algorithmic bytes (bench `traffic_note`)
+TRAFFIC_NOTES = {
+    "analysis_stream_kernel<256, 13, 8, 7, 2, false, 0>":
+        "the fused round trip's analysis also writes the synthesis stage-1 rows (153 MB per unit) "
+        "that the algorithmic count (input in + channelised product out) leaves out",
+}
+
+
 def traffic_for(workload, kernel, traffic):
     """(bytes, None) of the PMC record whose kernel IS the timed kernel, else (None, why)."""
     key = kernel_key(kernel)
@@ -520,6 +528,54 @@ def read_profile(lib, steps):
     return kern
 
 
+def capture_pipeline(torch, dev, pfb, pairs, inputs, n_dat, steps):
+    """The K steps as ONE captured two-stream software pipeline over D plan pairs: step i's
+    analysis half (pfb_roundtrip_analysis_execute) on stream A after step i-D's synthesis
+    released pair i mod D's stage-1 rows, its synthesis half
+    (pfb_roundtrip_synthesis_execute) on stream S after it — so step i+1's analysis runs
+    beside step i's synthesis.  Every step is one full round trip of one unit.  Returns the
+    graph's replay."""
+    D = len(pairs)
+
+    def enqueue(k):
+        sa = torch.cuda.current_stream(dev)
+        ss = torch.cuda.Stream(device=dev)
+        ss.wait_stream(sa)
+        ev_a = [torch.cuda.Event() for _ in range(k)]
+        ev_s = [torch.cuda.Event() for _ in range(k)]
+        for i in range(k):
+            p = i % D
+            a_, s_, c_, o_ = pairs[p]
+            if i >= D:
+                sa.wait_event(ev_s[i - D])
+            pfb.roundtrip_analysis(a_, s_, inputs[p], chan=c_)
+            ev_a[i].record(sa)
+            ss.wait_event(ev_a[i])
+            with torch.cuda.stream(ss):
+                pfb.roundtrip_synthesis(a_, s_, n_dat, out=o_)
+            ev_s[i].record(ss)
+        sa.wait_stream(ss)
+    pipe = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(pipe):
+        enqueue(steps)
+    torch.cuda.synchronize(dev)
+    return pipe.replay
+
+
+def capture_step(torch, dev, fn):
+    """One step captured as a HIP graph (after an eager run on a side stream)."""
+    graph = torch.cuda.CUDAGraph()
+    cs = torch.cuda.Stream(device=dev)
+    cs.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(cs):
+        fn()
+    torch.cuda.current_stream(dev).wait_stream(cs)
+    with torch.cuda.graph(graph):
+        fn()
+    torch.cuda.synchronize(dev)
+    return graph.replay
+
+
 def measure_c3(args, torch, dist, world, dev, pfb, lib, c3):
     """BASELINE configs[2]: SKA-Mid padded round trip — 4096 channels, OS
     8/7, 100 353 two-stage firls taps, 2^26 samples, Nf 512, Ov 128, tukey, deripple —
@@ -527,43 +583,73 @@ def measure_c3(args, torch, dist, world, dev, pfb, lib, c3):
     K timed steps between barrier + synchronize, then the same K with HIP events around
     every kernel (per-kernel durations and the roofline)."""
     taps = c3["taps"]
-    g = torch.Generator(device=dev).manual_seed(300)
-    x = (torch.complex(torch.randn((1, C3_N_DAT), device=dev, generator=g),
-                       torch.randn((1, C3_N_DAT), device=dev, generator=g)) / np.sqrt(2.0)).to(torch.complex64)
     win = pfb.PFBWindow().lookup["tukey"](C3_NF, C3_OV)
-    ana = pfb.AnalysisPlan(taps, C3_N_CHAN, OS_STR, "polyphase_analysis_padded", 1, dev.index or 0)
-    syn = pfb.SynthesisPlan(C3_N_CHAN, OS_STR, C3_NF, C3_OV, True, 1, True, taps, win, None, 1, dev.index or 0)
-    K = ana.output_length(C3_N_DAT)
-    n_out = syn.output_length(K)
-    chan = torch.empty((1, K, C3_N_CHAN), dtype=torch.complex64, device=dev)
-    out = torch.empty((1, n_out), dtype=torch.complex64, device=dev)
+    D = max(1, args.inflight)
+    # D plan pairs, each with its own unit (seed 300 + 7919 p), stage-1 rows, channelised and
+    # output buffers: consecutive steps are independent units, as in the C2 headline
+    pairs, inputs = [], []
+    for p in range(D):
+        g = torch.Generator(device=dev).manual_seed(300 + 7919 * p)
+        inputs.append((torch.complex(torch.randn((1, C3_N_DAT), device=dev, generator=g),
+                                     torch.randn((1, C3_N_DAT), device=dev, generator=g)) /
+                       np.sqrt(2.0)).to(torch.complex64))
+        ana = pfb.AnalysisPlan(taps, C3_N_CHAN, OS_STR, "polyphase_analysis_padded", 1, dev.index or 0)
+        syn = pfb.SynthesisPlan(C3_N_CHAN, OS_STR, C3_NF, C3_OV, True, 1, True, taps, win, None, 1,
+                                dev.index or 0)
+        K = ana.output_length(C3_N_DAT)
+        n_out = syn.output_length(K)
+        pairs.append((ana, syn, torch.empty((1, K, C3_N_CHAN), dtype=torch.complex64, device=dev),
+                      torch.empty((1, n_out), dtype=torch.complex64, device=dev)))
 
-    def step():
-        pfb.roundtrip(ana, syn, x, chan=chan, out=out)
-    for _ in range(max(1, args.warmup)):
-        step()
+    def step_of(p):
+        ana, syn, chan, out = pairs[p]
+        return lambda: pfb.roundtrip(ana, syn, inputs[p], chan=chan, out=out)
+    steps = [step_of(p) for p in range(D)]
+    for i in range(max(D, args.warmup)):
+        steps[i % D]()
     torch.cuda.synchronize(dev)
-    el = timed_region(args.steps, step, world, dist, lambda: torch.cuda.synchronize(dev))
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+    # timed region (`ms`): the K steps one at a time, one graph replay per step on one stream,
+    # the pairs' units in turn.  The captured two-stream pipeline of the C2 headline
+    # (`ms_pipelined`, D > 1) measured SLOWER for C3 (0.862 vs 0.810 ms, r06_v4): its FIR
+    # beside the Nf 512 synthesis contends for the CUs that kernel is bound by.
+    ones = [capture_step(torch, dev, st) for st in steps]
+    ctr = [0]
+
+    def one():
+        ones[ctr[0] % D]()
+        ctr[0] += 1
+    el = timed_region(args.steps, one, world, dist, sync)
+    el_pipe = None
+    if D > 1 and args.pipeline:
+        batch = capture_pipeline(torch, dev, pfb, pairs, inputs, C3_N_DAT, args.steps)
+        el_pipe = timed_region(1, batch, world, dist, sync)
+    # kernel-event region: the K steps eagerly with HIP events around every kernel (pair 0)
     lib.pfb_profile_reset()
     lib.pfb_profile_enable(1)
-    timed_region(args.steps, step, world, dist, lambda: torch.cuda.synchronize(dev))
+    timed_region(args.steps, steps[0], world, dist, sync)
     lib.pfb_profile_enable(0)
     kern = read_profile(lib, args.steps)
     lib.pfb_profile_reset()
     ms = el / args.steps * 1e3
     b_alg = 16.0 * (1.0 + 8.0 / 7.0) * C3_N_DAT  # x in + chan out + chan in + output out
     gbs = b_alg / (ms * 1e-3) / 1e9
+    K, n_out = pairs[0][2].shape[1], pairs[0][3].shape[1]
     res = {"workload": "C3 SKA-Mid padded round trip: 4096 ch, OS 8/7, %d two-stage firls taps, 2^26 "
-                       "samples, Nf 512, Ov 128, tukey, deripple; 1 single-pol unit" % len(taps),
+                       "samples, Nf 512, Ov 128, tukey, deripple; 1 single-pol unit per step" % len(taps),
            "ms": round(ms, 4), "value": round(C3_N_DAT / (ms * 1e-3) / 1e6, 2),
-           "unit": "complex Msamples/s", "steps": args.steps, "channelised_rows": K,
-           "output_samples": n_out,
+           "unit": "complex Msamples/s", "steps": args.steps,
+           "ms_pipelined": round(el_pipe / args.steps * 1e3, 4) if el_pipe else None,
+           "plan_pairs": D, "pipeline": False, "hip_graph": True,
+           "unit_seeds": [300 + 7919 * p for p in range(D)],
+           "channelised_rows": K, "output_samples": n_out,
            "roofline": {"bound": "hbm", "alg_bytes_per_step": b_alg, "achieved": round(gbs, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)},
            "kernels": kern}
-    del x, chan, out
-    ana.close()
-    syn.close()
+    for ana, syn, _, _ in pairs:
+        ana.close()
+        syn.close()
+    del pairs, inputs
     torch.cuda.empty_cache()
     return res
 
@@ -671,18 +757,7 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds, c3=No
     if args.graph:
         # the plans own all their device buffers after the warm-up, so the step is
         # capturable: one graph launch replays the step's kernels
-        runs = []
-        for s in steps_of:
-            graph = torch.cuda.CUDAGraph()
-            cs = torch.cuda.Stream(device=dev)
-            cs.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(cs):
-                s()
-            torch.cuda.current_stream(dev).wait_stream(cs)
-            with torch.cuda.graph(graph):
-                s()
-            torch.cuda.synchronize(dev)
-            runs.append(graph.replay)
+        runs = [capture_step(torch, dev, s) for s in steps_of]
     if D == 1:
         run = runs[0]
     else:
@@ -703,33 +778,8 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds, c3=No
 
     batch = None
     if args.pipeline and args.roundtrip and D > 1:
-        # two-stream software pipeline over the K steps, captured as ONE graph: step i's
-        # analysis half on stream A (after step i-D's synthesis released pair i mod D's
-        # stage-1 rows), its synthesis half on stream S after it — so step i+1's analysis
-        # runs beside step i's synthesis from the first step on
-        def enqueue(k):
-            sa = torch.cuda.current_stream(dev)
-            ss = torch.cuda.Stream(device=dev)
-            ss.wait_stream(sa)
-            ev_a = [torch.cuda.Event() for _ in range(k)]
-            ev_s = [torch.cuda.Event() for _ in range(k)]
-            for i in range(k):
-                p = i % D
-                a_, s_, c_, o_ = pairs[p]
-                if i >= D:
-                    sa.wait_event(ev_s[i - D])
-                pfb.roundtrip_analysis(a_, s_, inputs[p], chan=c_)
-                ev_a[i].record(sa)
-                ss.wait_event(ev_a[i])
-                with torch.cuda.stream(ss):
-                    pfb.roundtrip_synthesis(a_, s_, n_dat, out=o_)
-                ev_s[i].record(ss)
-            sa.wait_stream(ss)
-        pipe = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(pipe):
-            enqueue(args.steps)
-        torch.cuda.synchronize(dev)
-        batch = pipe.replay
+        # two-stream software pipeline over the K steps, captured as ONE graph
+        batch = capture_pipeline(torch, dev, pfb, pairs, inputs, n_dat, args.steps)
 
     # timed region: K steps, no instrumentation (value, ms_per_step)
     if batch is not None:
@@ -863,14 +913,25 @@ def report(args, res, world, workload, n_pol, n_dat, all_seeds):
         "kernels": kern,
     }
     traffic_all = pmc_traffic()
+
+    def with_traffic(kc, wl):
+        # PMC HBM bytes per launch of the same kernel in the same workload (pols included:
+        # the records are keyed by workload, whose name fixes the pols per launch)
+        kc["traffic"], _ = traffic_for(wl, kc.get("kernel"), traffic_all)
+        if kc["traffic"] and kc.get("alg_bytes_per_launch"):
+            kc["traffic_ratio"] = round(kc["traffic"] / kc["alg_bytes_per_launch"], 3)
+            note = TRAFFIC_NOTES.get(kernel_key(kc.get("kernel")) or "")
+            if kc["traffic_ratio"] > 1.6 and note:
+                kc["traffic_note"] = note
     for kc in kern.values():  # PMC HBM bytes per launch of every timed kernel class
-        kc["traffic"], _ = traffic_for(workload, kc.get("kernel"), traffic_all)
-    for key, wl in (("synthesis_only", "synthesis_only"), ("c3", "c3")):
+        with_traffic(kc, workload)
+    for key in ("synthesis_only", "c3"):
         sec = res.get(key)
         if sec is None:
             continue
+        wl = f"synthesis_only_p{n_pol}" if key == "synthesis_only" else key
         for kc in sec.get("kernels", {}).values():
-            kc["traffic"], _ = traffic_for(wl, kc.get("kernel"), traffic_all)
+            with_traffic(kc, wl)
             if kc["avg_ms"] > 0:
                 kc["achieved_GBs"] = round(kc["alg_bytes_per_launch"] / (kc["avg_ms"] * 1e-3) / 1e9, 1)
         out[key] = sec

@@ -1,7 +1,8 @@
 """A few steps of one workload for rocprofv3 --pmc passes (scripts/gpu_pmc_r05.sh):
 c2 = the fused C2 round trip (bench.py's step), c4 = the same for a dual-pol unit (bench.py
---gpus N > 1), c2syn = the standalone C2 synthesis
-(SynthesisPlan.execute of an HBM-resident channelised product), c3 = the SKA-Mid round trip.
+--gpus N > 1), c2syn / c4syn = the standalone synthesis (SynthesisPlan.execute of an
+HBM-resident channelised product) of a single- / dual-pol unit (bench.py's synthesis_only at
+--gpus 1 / > 1), c3 = the SKA-Mid round trip.
 Every kernel name then maps to one workload in profiles/pmc_traffic.json."""
 import argparse
 import os
@@ -15,7 +16,7 @@ sys.path[:0] = [os.path.join(REPO, "ska-pst-dsp-model_amd"), REPO]
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("c2", "c4", "c2syn", "c3"), required=True)
+    ap.add_argument("--workload", choices=("c2", "c4", "c2syn", "c4syn", "c3"), required=True)
     ap.add_argument("--steps", type=int, default=3)
     args = ap.parse_args()
     import torch
@@ -28,13 +29,13 @@ def main():
     else:
         taps = pfb.design_PFB_FIR_filter(256, "8/7", 12)
         N, nf, ov, var, n = 256, 256, 48, "polyphase_analysis", 1 << 24
-    n_pol = 2 if args.workload == "c4" else 1
+    n_pol = 2 if args.workload in ("c4", "c4syn") else 1
     x = (torch.complex(torch.randn((n_pol, n), device=dev, generator=g),
                        torch.randn((n_pol, n), device=dev, generator=g)) / np.sqrt(2)).to(torch.complex64)
     ana = pfb.AnalysisPlan(taps, N, "8/7", var, n_pol, 0)
     win = pfb.PFBWindow().lookup["tukey"](nf, ov)
     syn = pfb.SynthesisPlan(N, "8/7", nf, ov, True, 1, True, taps, win, None, n_pol, 0)
-    if args.workload == "c2syn":
+    if args.workload in ("c2syn", "c4syn"):
         chan = ana.execute(x).contiguous()
         torch.cuda.synchronize()
         for _ in range(args.steps):

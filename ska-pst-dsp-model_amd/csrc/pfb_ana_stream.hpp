@@ -253,7 +253,8 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
 
 template <int N, int P, int NU, int DE, int ZOUT, bool LCBF = false, int GS = 0>
 __global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
-  analysis_stream_body<N, P, NU, DE, ZOUT, LCBF, GS>(a, blockIdx.y, xcd_tile(blockIdx.x, gridDim.x), gridDim.x);
+  const int w = a.linear ? (int)blockIdx.x : xcd_tile(blockIdx.x, gridDim.x);
+  analysis_stream_body<N, P, NU, DE, ZOUT, LCBF, GS>(a, blockIdx.y, w, gridDim.x);
 }
 
 }  // namespace pfb

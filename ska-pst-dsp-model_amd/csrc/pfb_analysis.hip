@@ -682,9 +682,18 @@ static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
   // buffer descriptor: huge single series get more, shorter ranges
   const int64_t fit_steps = (kRsrcMaxBytes / (8 * N) - SH::WIN) / SH::NEW;
   wgs = std::max(wgs, (n_steps + fit_steps - 1) / fit_steps);
+  // (PFB_ANA_STEPS=S: S steps per workgroup, ceil(n_steps / S) workgroups instead of the
+  // resident count; PFB_ANA_LINEAR=1: linear workgroup order — experiments A/B)
+  AnalysisArgs b = a;
+  if constexpr (kExperiments) {
+    static const int steps = knob("PFB_ANA_STEPS") ? std::atoi(knob("PFB_ANA_STEPS")) : 0;
+    static const int lin = knob("PFB_ANA_LINEAR") ? std::atoi(knob("PFB_ANA_LINEAR")) : -1;
+    if (steps > 0) wgs = std::max(wgs, (n_steps + steps - 1) / steps);
+    if (lin >= 0) b.linear = lin;
+  }
   if (wgs > INT32_MAX) return hipErrorInvalidValue;
   dim3 grid((unsigned)wgs, (unsigned)a.n_pol);
-  return launch_kernel(kern, grid, dim3(NT), SH::lds_bytes, s, a);
+  return launch_kernel(kern, grid, dim3(NT), SH::lds_bytes, s, b);
 }
 
 // streaming kernel for the SKA-Low shapes (N = 256, Bunton); 0 = not compiled
@@ -804,6 +813,7 @@ hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
     RowFftArgs rz{a.z + a.row0 * a.N, a.z_pol_stride, a.out + a.row0 * a.N, a.out_pol_stride, rows, a.zrev,
                   nullptr, a.twN, 1.0f / (float)a.N, 0, 0, 0, a.K_total};
     rz.in_run = a.zblk == 2 ? 1 : 0;
+    rz.rev = a.zrev != nullptr ? 1 : 0;  // (zrev is always the index reversal, pfb_api.hip)
     if (a.variant == kBunton) return dispatch_row_fft<-1>(a.N, rz, a.n_pol, s);
     return dispatch_row_fft<+1>(a.N, rz, a.n_pol, s);
   }

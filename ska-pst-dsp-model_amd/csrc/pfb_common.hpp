@@ -281,6 +281,8 @@ struct RowFftArgs {
   int zs = 0;        // output rows in runs of 2^zs per column (RowStore::zs)
   int nt = 1;        // RowStore::nt (the 4096-point kernel's rows are always nontemporal)
   int in_run = 0;    // input rows in 2-row runs per column (z_index), the SKA-Mid stage-1 rows
+  int rev = 0;       // perm is the index reversal (N - i) mod N (the 4096-point pair kernel
+                     // computes it instead of holding 16 column offsets per thread)
 };
 
 template <int N>

@@ -88,6 +88,9 @@ struct AnalysisArgs {
   // other than `pre`), spread over the grid before the main loop: no separate copy launch
   float2* carry_out;
   int64_t carry_src, carry_n, carry_pol_stride;
+  // workgroup -> step range order: 0 XCD-aware (xcd_tile), 1 linear (blockIdx.x: the
+  // dispatcher's order is the rows' order, so the chip's loads in flight stay in one window)
+  int linear = 0;
 };
 // SKA-Low CBF PST filterbank through the streaming analysis kernel (pfb_analysis.hip)
 hipError_t launch_lowcbf_stream(const AnalysisArgs& a, hipStream_t s);
@@ -153,6 +156,9 @@ struct SynthBlockArgs {
   const float* fir_g;
   int64_t fir_q0;
   int fir_nu, fir_de, fir_pe;
+  // wave kernels: workgroup -> (block range, phase group) order, 0 XCD-aware (xcd_tile), 1
+  // linear (blockIdx.x: consecutive workgroups are the phase groups of one block range)
+  int linear = 0;
 };
 
 // Synthesis with a non-identity spectral taper (pfb_spectral.hip): blocks [b0, b0 + nb)

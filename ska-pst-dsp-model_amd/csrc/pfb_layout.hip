@@ -329,18 +329,18 @@ hipError_t stats_buffer(double** out) {
   return hipSuccess;
 }
 
-// Bandwidth probe (the achievable HBM rate beside the 8 TB/s spec): each
-// thread moves four float4, the four loads issued before the four stores.
-__global__ void __launch_bounds__(TPB) copy_kernel(const float4* __restrict__ src,
-                                                   float4* __restrict__ dst, int64_t n4) {
-  const int64_t base = (int64_t)blockIdx.x * TPB * 4 + threadIdx.x;
-  float4 v[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-    if (base + u * TPB < n4) v[u] = src[base + u * TPB];
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-    if (base + u * TPB < n4) dst[base + u * TPB] = v[u];
+// Bandwidth probe (the achievable HBM rate beside the 8 TB/s spec): one float4
+// per thread, nontemporal load and store, one-shot grid of 256-thread workgroups.  Round 6
+// (scripts/copy_probe.hip, profiles/r06_copy_probe.jsonl, 2 GiB -> 2 GiB): this shape moves
+// 6.5-6.6 TB/s (read + write); four float4 per thread 5.6-5.8, persistent grid-stride or
+// contiguous-range loops 4.7-5.5 — the dispatcher's in-order workgroups keep the chip's
+// requests in flight in one narrow window of addresses.  (Round 5's four-per-thread form
+// measured 5.5 TB/s, which made every kernel look closer to the ceiling than it was.)
+typedef float copy_v4f __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(TPB) copy_kernel(const copy_v4f* __restrict__ src,
+                                                   copy_v4f* __restrict__ dst, int64_t n4) {
+  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i < n4) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
 // n_pol rows of n samples, dst + q dps <- src + q sps (device to device): the strided
@@ -478,10 +478,11 @@ pfb_status pfb_device_copy(void* dst, const void* src, int64_t n_bytes, void* st
     return bad("pfb_device_copy: 16-B aligned pointers and a multiple of 64 bytes required");
   const int64_t n4 = n_bytes / 16;
   if (!n4) return PFB_OK;
-  const int64_t per_block = (int64_t)TPB * 4;
-  const dim3 g((unsigned)((n4 + per_block - 1) / per_block));
-  hipLaunchKernelGGL(copy_kernel, g, TPB, 0, (hipStream_t)stream, (const float4*)src,
-                     (float4*)dst, n4);
+  const int64_t blocks = (n4 + TPB - 1) / TPB;
+  if (blocks > INT32_MAX) return bad("pfb_device_copy: more than 2^31 - 1 workgroups");
+  const dim3 g((unsigned)blocks);
+  hipLaunchKernelGGL(copy_kernel, g, TPB, 0, (hipStream_t)stream, (const copy_v4f*)src,
+                     (copy_v4f*)dst, n4);
   LCHK(hipGetLastError());
   return PFB_OK;
 }

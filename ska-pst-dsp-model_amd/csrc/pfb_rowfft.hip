@@ -49,6 +49,72 @@ __device__ __forceinline__ void r4k_twiddles(const float2* t, int k, int stride,
   });
 }
 
+// One row held as v[r] = element tid + 256 r (pass-1 input order): the three radix-16 passes
+// through the LDS row; on return v[r] = output element tid + 256 r.  Opens with the barrier
+// that orders it after the previous row's pass 3 (and the tables' staging).
+template <int DIR>
+__device__ __forceinline__ void r4k_fft(float2 (&v)[16], float2* row, const float2* t2, const float2* t3, int tid) {
+  const int k2 = tid & 15;
+  const int st2 = (tid >> 4) * 256 + k2;     // pass-2 output base (j / 16) 256 + k
+  __syncthreads();  // tables staged / the previous row's pass 3 is done with the LDS row
+  // pass 1 (NS 1): no twiddles, outputs tid 16 + r
+  sdft<16, DIR>(v);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) row[kR4kA * r + tid] = v[r];  // layout A
+  __syncthreads();
+  // pass 2 (NS 16): k = tid mod 16, twiddles w^r, r = 1..15, of m = 16 k
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = row[kR4kA * k2 + (tid >> 4) + 16 * r];  // element tid + 256 r
+  {
+    float2 w[16];
+    r4k_twiddles<DIR>(t2, k2, 16, w);
+    static_for<1, 16>([&](auto r) { v[r] = cmul(v[r], w[r]); });
+  }
+  sdft<16, DIR>(v);
+  __syncthreads();  // every pass-2 load done before the in-place stores
+#pragma unroll
+  for (int r = 0; r < 16; ++r) row[st2 + 16 * r] = v[r];  // layout B
+  __syncthreads();
+  // pass 3 (NS 256): k = tid, twiddles of m = k; outputs tid + 256 r
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = row[tid + 256 * r];
+  {
+    float2 w[16];
+    r4k_twiddles<DIR>(t3, tid, 256, w);
+    static_for<1, 16>([&](auto r) { v[r] = cmul(v[r], w[r]); });
+  }
+  sdft<16, DIR>(v);
+}
+
+// Output row rw (row_base + rw, circularly shifted by -sds mod n_total when remap: the padded
+// variant's time shift, RowStore's rule) of a [row][N] product -> HBM.
+__device__ __forceinline__ void r4k_store_row(const float2 (&v)[16], int tid, const RowFftArgs& a, float2* out,
+                                              int64_t rw) {
+  int64_t t = a.row_base + rw;
+  if (a.remap) {
+    t -= a.sds;
+    while (t < 0) t += a.n_total;
+  }
+  // (t is uniform, but the uniformity analysis loses it through the wrap loop: without the
+  // read-first-lane every store became a one-trip waterfall loop over the descriptor)
+  t = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)t >> 32)) << 32) |
+                __builtin_amdgcn_readfirstlane((uint32_t)t));
+  const __amdgpu_buffer_rsrc_t os = make_rsrc(out + t * 4096, (uint32_t)(4096 * 8));
+  const uint32_t lane_off = (uint32_t)tid * 8u;
+  static_for<0, 16>([&](auto rv) {
+    constexpr int r = decltype(rv)::value;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v[r], a.scale)), os, lane_off,
+                                          r * 2048, kNtRow ? 2 : 0);
+  });
+}
+
+template <int DIR>
+__device__ __forceinline__ void r4k_row(float2 (&v)[16], float2* row, const float2* t2, const float2* t3,
+                                        int tid, const RowFftArgs& a, float2* out, int64_t rw) {
+  r4k_fft<DIR>(v, row, t2, t3, tid);
+  r4k_store_row(v, tid, a, out, rw);
+}
+
 // (buffer loads / stores: one descriptor per row, the lane's byte offset tid * 8 and the
 // register's r * 2048 as a scalar offset — no 64-bit address per register: <= 168 VGPRs,
 // 3 workgroups per CU)
@@ -106,59 +172,125 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void ro
   };
   load_row(q0);
   vm_drain();
-  const int k2 = tid & 15;
-  const int st2 = (tid >> 4) * 256 + k2;     // pass-2 output base (j / 16) 256 + k
 #pragma unroll 1
   for (int64_t rw = q0; rw < q1; ++rw) {
     float2 v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = GAIN ? cscale(pf[r], g[GAIN ? r : 0]) : pf[r];
     load_row(min(rw + 1, q1 - 1));  // unconditional: past the end re-reads the last row
-    __syncthreads();  // tables staged / the previous row's pass 3 is done with the LDS row
-    // pass 1 (NS 1): no twiddles, outputs tid 16 + r
-    sdft<16, DIR>(v);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) row[kR4kA * r + tid] = v[r];  // layout A
-    __syncthreads();
-    // pass 2 (NS 16): k = tid mod 16, twiddles w^r, r = 1..15, of m = 16 k
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = row[kR4kA * k2 + (tid >> 4) + 16 * r];  // element tid + 256 r
-    {
-      float2 w[16];
-      r4k_twiddles<DIR>(t2, k2, 16, w);
-      static_for<1, 16>([&](auto r) { v[r] = cmul(v[r], w[r]); });
-    }
-    sdft<16, DIR>(v);
-    __syncthreads();  // every pass-2 load done before the in-place stores
-#pragma unroll
-    for (int r = 0; r < 16; ++r) row[st2 + 16 * r] = v[r];  // layout B
-    __syncthreads();
-    // pass 3 (NS 256): k = tid, twiddles of m = k; outputs tid + 256 r -> HBM
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = row[tid + 256 * r];
-    {
-      float2 w[16];
-      r4k_twiddles<DIR>(t3, tid, 256, w);
-      static_for<1, 16>([&](auto r) { v[r] = cmul(v[r], w[r]); });
-    }
-    sdft<16, DIR>(v);
-    // output row: row_base + rw, circularly shifted by -sds mod n_total (the padded
-    // variant's time shift, RowStore's rule)
-    int64_t t = a.row_base + rw;
-    if (a.remap) {
-      t -= a.sds;
-      while (t < 0) t += a.n_total;
-    }
-    // (t is uniform, but the uniformity analysis loses it through the wrap loop: without the
-    // read-first-lane every store became a one-trip waterfall loop over the descriptor)
-    t = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)t >> 32)) << 32) |
-                  __builtin_amdgcn_readfirstlane((uint32_t)t));
-    const __amdgpu_buffer_rsrc_t os = make_rsrc(out + t * N, (uint32_t)(N * 8));
+    r4k_row<DIR>(v, row, t2, t3, tid, a, out, rw);
+  }
+}
+
+// Round 6: rows in PAIRS, one pair per workgroup.  RUN (in_run: the SKA-Mid round trip's
+// stage-1 rows as the FIR writes them, 2-row runs per column): each lane loads element i of
+// both rows with one 16-B buffer load, so the run's 128-B lines cross the memory side once
+// (the one-row kernel loaded 8 B of every 16 and re-fetched the partner's lines one row
+// later: 913 MB read for 613 MB of rows; 625 MB now, r06 PMC).  !RUN: rows
+// [row][N], two 8-B loads per element.  Row 2p is transformed from the first halves while
+// row 2p + 1 waits in registers.  REV: the padded variant's index reversal (column (N - i)
+// mod N for element i) computed from the lane (element i = tid + 256 r: r >= 1 reads column
+// 4096 - 256 r - tid, one lane base (255 - tid) and a scalar offset; r = 0 its own lane
+// offset) — 2 registers instead of the 16 column offsets of the generic permutation.  OZS:
+// the output in 2-row runs (RowStore::zs = 1, the Nf 512 synthesis' stage-1 layout; row A's
+// results held until row B's, one 16-B store per element).  Same passes and tables as the
+// one-row kernel: bit-identical.
+// SCHED (which pairs a workgroup takes): 0 a contiguous range (XCD-aware order), 1 grid-stride
+// from blockIdx.x, 2 one pair per workgroup (grid = pairs) — the default: the dispatcher hands
+// out pairs in row order, so the chip's loads in flight stay in one narrow window of the
+// rows; 224 vs 262 us per C3 launch (persistent ranges), 243 grid-stride
+// (profiles/r06_v3_rowfft_sched_ab.log).  The same holds for a plain float4 copy: one 16-B
+// load + store per thread, one-shot grid, 6.6 TB/s; persistent grid-stride or range loops
+// 4.7-5.5 TB/s (scripts/copy_probe.hip, profiles/r06_copy_probe.jsonl).
+template <int DIR, bool REV, int SCHED, bool RUN = true, bool OZS = false>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void row_fft4096_pair_kernel(RowFftArgs a) {
+  constexpr int N = 4096;
+  constexpr uint32_t ES = RUN ? 16u : 8u;  // bytes between elements i and i + 1 of a row
+  extern __shared__ __attribute__((aligned(16))) float2 smem[];
+  const int pol = blockIdx.y;
+  const int64_t np = (a.n_rows + 1) >> 1;
+  int64_t p0, p1, pstep = 1;
+  if constexpr (SCHED == 0) {
+    const int wg = xcd_tile(blockIdx.x, gridDim.x);
+    p0 = np * wg / gridDim.x;
+    p1 = np * (wg + 1) / gridDim.x;
+  } else if constexpr (SCHED == 1) {
+    p0 = blockIdx.x;
+    p1 = np;
+    pstep = gridDim.x;
+  } else {
+    p0 = blockIdx.x;
+    p1 = min(p0 + 1, np);
+  }
+  if (p0 >= p1) return;  // uniform per workgroup
+  const int tid = threadIdx.x;
+  float2* row = smem;
+  float2* t2 = smem + kR4kRow;
+  float2* t3 = t2 + kR4kTw2;
+  for (int e = tid; e < kR4kTw3; e += NT) {
+    const int pp = e >> 8, k = e & 255;
+    t3[e] = a.tw[(k << pp) & (N - 1)];
+    if (e < kR4kTw2) t2[e] = a.tw[((e & 15) << ((e >> 4) + 4)) & (N - 1)];
+  }
+  const float2* in = a.in + pol * a.in_pol_stride;
+  float2* out = a.out + pol * a.out_pol_stride;
+  const uint32_t lane_a = REV ? (uint32_t)(255 - tid) * ES : (uint32_t)tid * ES;
+  const uint32_t lane_0 = REV ? (tid ? (uint32_t)(N - tid) * ES : 0u) : lane_a;
+  v4u pf[16];
+  auto load_pair = [&](int64_t pp) {
+    // (!RUN: the last pair of an odd row count has no row B — its loads leave the range)
+    const uint32_t nrec = RUN ? (uint32_t)(N * 16) : (2 * pp + 1 < a.n_rows ? 2u : 1u) * (uint32_t)(N * 8);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc_u(in + pp * 2 * N, nrec);
     static_for<0, 16>([&](auto rv) {
       constexpr int r = decltype(rv)::value;
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, cscale(v[r], a.scale)), os, lane_off,
-                                            r * 2048, kNtRow ? 2 : 0);
+      constexpr int soff = r == 0 ? 0 : REV ? (3841 - 256 * r) * (int)ES : r * 256 * (int)ES;
+      const uint32_t lo = r == 0 ? lane_0 : lane_a;
+      if constexpr (RUN) {
+        pf[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, lo, soff, kNtlRow ? 2 : 0);
+      } else {
+        const v2u x0 = __builtin_amdgcn_raw_buffer_load_b64(rs, lo, soff, kNtlRow ? 2 : 0);
+        const v2u x1 = __builtin_amdgcn_raw_buffer_load_b64(rs, lo, soff + N * 8, kNtlRow ? 2 : 0);
+        pf[r] = v4u{x0.x, x0.y, x1.x, x1.y};
+      }
     });
+  };
+  load_pair(p0);
+  vm_drain();
+#pragma unroll 1
+  for (int64_t pp = p0; pp < p1; pp += pstep) {
+    float2 v[16], h[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const v4f x = __builtin_bit_cast(v4f, pf[r]);
+      v[r] = make_float2(x.x, x.y);
+      h[r] = make_float2(x.z, x.w);
+    }
+    if constexpr (OZS) {
+      // both rows transformed, then element i of rows (2p, 2p + 1) as one 16-B store into
+      // run p (row_base even, no remap: launch_row_fft_t checks)
+      r4k_fft<DIR>(v, row, t2, t3, tid);
+      if constexpr (SCHED != 2) load_pair(pp + pstep < p1 ? pp + pstep : pp);
+      r4k_fft<DIR>(h, row, t2, t3, tid);
+      const int64_t run = (a.row_base >> 1) + pp;
+      const __amdgpu_buffer_rsrc_t os = make_rsrc_u(out + run * 2 * N, (uint32_t)(N * 16));
+      auto st = [&](auto aux) {
+        static_for<0, 16>([&](auto rv) {
+          constexpr int r = decltype(rv)::value;
+          const float2 x0 = cscale(v[r], a.scale), x1 = cscale(h[r], a.scale);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{x0.x, x0.y, x1.x, x1.y}), os,
+                                                 (uint32_t)tid * 16u, r * 4096, decltype(aux)::value);
+        });
+      };
+      // (RowStore::nt: the default policy for rows the synthesis reads right after from the
+      // Infinity Cache; uniform)
+      if (a.nt && kNtRow) st(std::integral_constant<int, 2>{});
+      else st(std::integral_constant<int, 0>{});
+    } else {
+      r4k_row<DIR>(v, row, t2, t3, tid, a, out, 2 * pp);
+      if constexpr (SCHED != 2)
+        load_pair(pp + pstep < p1 ? pp + pstep : pp);  // unconditional: past the end re-reads this pair
+      if (2 * pp + 1 < a.n_rows) r4k_row<DIR>(h, row, t2, t3, tid, a, out, 2 * pp + 1);  // (uniform)
+    }
   }
 }
 
@@ -170,6 +302,27 @@ static hipError_t launch_row_fft4096(const RowFftArgs& r, int n_pol, hipStream_t
   const int64_t wgs = (int64_t)cu_count() * per_cu;
   dim3 grid((unsigned)std::max<int64_t>(1, wgs / n_pol), (unsigned)n_pol);
   return launch_kernel(kern, grid, dim3(NT), kR4kLds, s, r);
+}
+
+template <int DIR, bool REV, int SCHED, bool RUN, bool OZS>
+static hipError_t launch_r4k_pair(const RowFftArgs& r, int n_pol, hipStream_t s, int per_cu) {
+  auto kern = row_fft4096_pair_kernel<DIR, REV, SCHED, RUN, OZS>;
+  hipError_t e = set_lds(kern, kR4kLds);
+  if (e != hipSuccess) return e;
+  const int64_t wgs = SCHED == 2 ? (r.n_rows + 1) / 2 : (int64_t)cu_count() * per_cu / n_pol;
+  if (wgs > INT32_MAX) return hipErrorInvalidValue;
+  dim3 grid((unsigned)std::max<int64_t>(1, wgs), (unsigned)n_pol);
+  return launch_kernel(kern, grid, dim3(NT), kR4kLds, s, r);
+}
+template <int DIR, bool REV, bool RUN, bool OZS>
+static hipError_t launch_row_fft4096_pair(const RowFftArgs& r, int n_pol, hipStream_t s, int per_cu) {
+  // (PFB_ROWFFT_SCHED: 0 ranges, 1 grid-stride, 2 one pair per workgroup — experiments A/B)
+  static const int sched = knob("PFB_ROWFFT_SCHED") ? std::atoi(knob("PFB_ROWFFT_SCHED")) : 2;
+  if constexpr (kExperiments) {
+    if (sched == 0) return launch_r4k_pair<DIR, REV, 0, RUN, OZS>(r, n_pol, s, per_cu);
+    if (sched == 1) return launch_r4k_pair<DIR, REV, 1, RUN, OZS>(r, n_pol, s, per_cu);
+  }
+  return launch_r4k_pair<DIR, REV, 2, RUN, OZS>(r, n_pol, s, per_cu);
 }
 
 template <int N, int DIR, bool PERM, bool GAIN>
@@ -188,6 +341,19 @@ static hipError_t launch_row_fft_t(const RowFftArgs& r, int n_pol, hipStream_t s
     static const bool k4 = !(knob("PFB_ROWFFT_4K") && std::atoi(knob("PFB_ROWFFT_4K")) == 0);
     static const int wpc = knob("PFB_ROWFFT_WPC") ? std::atoi(knob("PFB_ROWFFT_WPC")) : 0;
     const int per_cu4 = wpc > 0 ? wpc : (int)std::max<size_t>(1, std::min<size_t>(3, (160 * 1024) / kR4kLds));
+    // the pair kernel (no per-channel gain, no permutation but the padded index reversal;
+    // output rows [row][N], or 2-row runs from an even first row without the time shift);
+    // PFB_ROWFFT_PAIR=0: the one-row kernel (A/B)
+    static const bool no_pair = knob("PFB_ROWFFT_PAIR") && std::atoi(knob("PFB_ROWFFT_PAIR")) == 0;
+    if constexpr (!GAIN) {
+      const bool ozs = r.zs == 1 && !r.remap && (r.row_base & 1) == 0 && (r.n_rows & 1) == 0;
+      if (!off && k4 && !no_pair && (!PERM || r.rev) && (r.zs == 0 || ozs) && r.n_rows >= 2) {
+        if (r.in_run) return ozs ? launch_row_fft4096_pair<DIR, PERM, true, true>(r, n_pol, s, per_cu4)
+                                 : launch_row_fft4096_pair<DIR, PERM, true, false>(r, n_pol, s, per_cu4);
+        return ozs ? launch_row_fft4096_pair<DIR, PERM, false, true>(r, n_pol, s, per_cu4)
+                   : launch_row_fft4096_pair<DIR, PERM, false, false>(r, n_pol, s, per_cu4);
+      }
+    }
     if (!off && k4 && r.zs == 0 && r.n_rows >= 4 * (int64_t)cu_count() * per_cu4)
       return launch_row_fft4096<DIR, PERM, GAIN>(r, n_pol, s, per_cu4);
     if (!off && r.n_rows >= 4 * wgs) {

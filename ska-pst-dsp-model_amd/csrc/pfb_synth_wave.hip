@@ -77,9 +77,17 @@ static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
   static const int env_wpc = knob("PFB_WAVE_PER_CU") ? std::atoi(knob("PFB_WAVE_PER_CU")) : 0;  // A/B
   if (env_wpc > 0) per_cu = env_wpc;
   int ranges = std::max(1, cu_count() * per_cu / (groups * a.n_pol));
+  // (PFB_WAVE_RANGES=R: R block ranges; PFB_WAVE_LINEAR=1: linear order — experiments A/B)
+  SynthBlockArgs b = a;
+  if constexpr (kExperiments) {
+    static const int env_r = knob("PFB_WAVE_RANGES") ? std::atoi(knob("PFB_WAVE_RANGES")) : 0;
+    static const int lin = knob("PFB_WAVE_LINEAR") ? std::atoi(knob("PFB_WAVE_LINEAR")) : -1;
+    if (env_r > 0) ranges = env_r;
+    if (lin >= 0) b.linear = lin;
+  }
   ranges = std::min(ranges, a.n_blocks);
   dim3 grid((unsigned)(groups * ranges), (unsigned)a.n_pol);
-  return launch_kernel(kern, grid, dim3(kWgThreads), kLdsB, s, a);
+  return launch_kernel(kern, grid, dim3(kWgThreads), kLdsB, s, b);
 }
 
 // the flat-window choice of the stored-rows kernel (PFB_WAVE_WFLAT=0: off, experiments A/B)

@@ -420,7 +420,7 @@ template <int RW, bool SPANS, int DK, bool XW = false, class FIRV = NoFir, bool 
 __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(3)))
 void synth_wave_kernel(SynthBlockArgs a) {
   const int groups = a.N / kCols;
-  const int lt = xcd_tile(blockIdx.x, gridDim.x);
+  const int lt = a.linear ? (int)blockIdx.x : xcd_tile(blockIdx.x, gridDim.x);
   const int rr = lt / groups;
   const int Rg = gridDim.x / groups;
   const int b_begin = (int)((int64_t)a.n_blocks * rr / Rg);

@@ -154,7 +154,7 @@ void synth_wave512_kernel(SynthBlockArgs a) {
   const int lane = tid & 63;
   const int N = a.N;
   const int groups = N / kW5Cols;
-  const int lt = xcd_tile(blockIdx.x, gridDim.x);
+  const int lt = a.linear ? (int)blockIdx.x : xcd_tile(blockIdx.x, gridDim.x);
   const int rr = lt / groups;
   const int Rg = gridDim.x / groups;
   const int b_begin = (int)((int64_t)a.n_blocks * rr / Rg);
@@ -407,8 +407,13 @@ static hipError_t launch_w5(const SynthBlockArgs& a, hipStream_t s) {
   static const int env_r = knob("PFB_W5_RANGES") ? std::atoi(knob("PFB_W5_RANGES")) : 0;  // A/B
   if (env_r > 0) ranges = env_r;
   ranges = std::min(ranges, a.n_blocks);
+  SynthBlockArgs b = a;
+  if constexpr (kExperiments) {  // (PFB_W5_LINEAR=1: linear workgroup order, A/B)
+    static const int lin = knob("PFB_W5_LINEAR") ? std::atoi(knob("PFB_W5_LINEAR")) : -1;
+    if (lin >= 0) b.linear = lin;
+  }
   dim3 grid((unsigned)(groups * ranges), (unsigned)a.n_pol);
-  return launch_kernel(kern, grid, dim3(kW5Threads), lds, s, a);
+  return launch_kernel(kern, grid, dim3(kW5Threads), lds, s, b);
 }
 
 hipError_t launch_synth_wave512(const SynthBlockArgs& a, hipStream_t s) {
