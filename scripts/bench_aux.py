@@ -142,6 +142,25 @@ def twostage(torch, pfb, noise, reps):
     emit("TwoStageFilterBank 256x256 (corner turn + gather path)", ms, 16 * (1 + 8 / 7) * (1 << 24),
          msamples_per_s=round((1 << 24) / ms / 1e3, 1),
          note="bytes: the two analyses' input+output, excluding the corner turn and gather")
+    del xs, ts, ts2, ts3
+    # BASELINE configs[2]'s cascade: both stages polyphase_analysis_padded (test.config.json
+    # `mid`, TwoStageFilterBank.m:27,51-52) — the SKA-Mid stage 1 (4096 ch, 8/7, 100 353 taps)
+    # into a 16-ch padded stage 2 over every coarse channel, critical, one 2^26-sample unit
+    taps1 = pfb.design_PFB_FIR_filter_two_stage(4096, "8/7", 28)
+    taps2 = pfb.design_PFB_FIR_filter(16, "8/7", 10)
+
+    def pcfg(t, n):
+        return dict(analysis_function="polyphase_analysis_padded", filt_coeff=t, channels=n, os_factor="8/7")
+    nm = 1 << 26
+    xm = noise(1, 1, nm)
+    tm = pfb.TwoStageFilterBank(pcfg(taps1, 4096)).set_stage2_config(pcfg(taps2, 16))
+    tm.critical = 1
+    tm.execute(xm)
+    ms = timeit(torch, lambda: tm.execute(xm), reps)
+    emit("TwoStageFilterBank SKA-Mid 4096x16 padded (stream call)", ms, 16 * (1 + 8 / 7) * nm,
+         msamples_per_s=round(nm / ms / 1e3, 1),
+         note="both stages polyphase_analysis_padded; bytes: the two analyses' input+output")
+    del xm, tm
 
 
 def cpu_baselines(pfb):

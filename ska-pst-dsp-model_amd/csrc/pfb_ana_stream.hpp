@@ -188,7 +188,7 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
     const int64_t kz = k0 - a.z_row0;
     const __amdgpu_buffer_rsrc_t zb =
         make_rsrc(ZOUT >= 2 ? a.z + pol * a.z_pol_stride + max(kz, (int64_t)0) * N : opol,
-                  (ZOUT >= 2 && kz >= 0) ? (uint32_t)(N * T * 8) : 0u);
+                  (ZOUT >= 2 && kz >= 0 && !(tmask(a.timing_mask) & 4)) ? (uint32_t)(N * T * 8) : 0u);
     static_for<0, NU>([&](auto sv) {
       constexpr int s = decltype(sv)::value;
       static_for<0, QS>([&](auto qv) {
@@ -241,7 +241,8 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
                                                        a.sel_split, a.sel_shift, a.sel_n, N, (float)N);
       block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
     } else {
-      const BufRowStore st = BufRowStore::rows(opol, k0, T, a.row0, a.K, N, (float)N);
+      // (timing mask bit 1, experiments build: no channelised stores)
+      const BufRowStore st = BufRowStore::rows(opol, k0, T, a.row0, (tmask(a.timing_mask) & 2) ? k0 : a.K, N, (float)N);
       block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
     }
 #pragma unroll

@@ -126,6 +126,15 @@ struct AnalysisStore {
 // the descriptor's base are written, others dropped by the hardware (an out-of-range
 // offset) — no branch per store, so the wave's vmcnt count stays path-independent and
 // a later wait for a prefetch never has to wait for these stores too.
+// Workgroup barrier of the wave synthesis kernels' block loops; TM bit 3 (a compile-time
+// timing variant of the experiments build, results invalid) makes it a wave barrier — the
+// barriers' share of a block's time
+template <int TM>
+__device__ __forceinline__ void wave_wg_sync() {
+  if constexpr ((TM & 8) != 0) __builtin_amdgcn_wave_barrier();
+  else __syncthreads();
+}
+
 struct BufRowStore {
   static constexpr bool kIsLds = false;
   __amdgpu_buffer_rsrc_t r;

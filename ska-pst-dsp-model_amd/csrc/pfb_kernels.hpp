@@ -47,7 +47,8 @@ struct AnalysisArgs {
   const float2* twN;       // e^{-2 pi i m / N}, m < N (device)
   float2* scratch;         // generic path: [pol][K - row0][N] (device) or null
   int timing_mask;         // timing experiments only (PFB_ANA_MASK, results invalid): bit0 no
-                           // input loads (streaming kernel)
+                           // input loads, bit1 no channelised stores, bit2 no Z stores
+                           // (streaming kernel)
   // Round trip only (pfb_roundtrip_execute): when z is set, every output row k >= z_row0
   // is also transformed by the synthesis stage-1 channel IFFT (the exact computation
   // row_fft_kernel<N, +1> performs on the stored row) into z[pol][k - z_row0][t0].
@@ -143,7 +144,9 @@ struct SynthBlockArgs {
   int no_reuse;            // 1: re-read the 2 Ov overlap rows from HBM (PFB_SYNTH_NO_REUSE, A/B only)
   int xcd;                 // 1: XCD-aware workgroup -> (phase group, range) order (PFB_SYNTH_XCD)
   int timing_mask;         // experiments build only (PFB_TIMING_MASK, results invalid): bit0
-                           // drop Z loads, bit1 drop output stores, bit2 drop tw4 loads
+                           // drop Z loads, bit1 drop output stores, bit2 drop tw4 loads; wave
+                           // kernels: bit3 wave barriers for the block loop's workgroup
+                           // barriers, bit4 a uniform twiddle for the LDS twiddle tables
   int zblk;                // Z layout of AnalysisArgs::zblk (0/1 rows, else ZB-row runs)
   // Recomputed stage-1 rows (the Nf = 256 round trip, synth_wave_kernel with fir_x set): the
   // analysis writes no Z; the synthesis evaluates each row it needs as N^2 x the streaming

@@ -69,6 +69,31 @@ static hipError_t launch_wave_t(const SynthBlockArgs& a, hipStream_t s) {
     if (prio == 32) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 32>;
     if (prio == 33) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, 33>;
   }
+  if constexpr (!FIRV::kOn && RW <= 14) {
+    // stored stage-1 rows with L_ov = 3 RW N (keep 160, Ov 48): the kept-register stores
+    // (V 1, round 6, pfb_synth_wave.hpp): 134 instead of 164 VGPRs, 10 stores a block instead
+    // of 16, no load or store wait inside the block.  Measured equal to the old kernel
+    // (63.2-64.8 vs 64.0-65.6 us on C2, interleaved); the ping-pong (2) and deferred-store (4)
+    // forms gain nothing on top (profiles/r06_v5_c2_wave_v_ab.jsonl).  PFB_WAVE_V=0/1/3/5/7:
+    // the variants (experiments build A/B)
+    int v = 1;
+    if constexpr (kExperiments) {
+      static const int ev = knob("PFB_WAVE_V") ? std::atoi(knob("PFB_WAVE_V")) : -1;
+      if (ev >= 0) v = ev;
+    }
+    if (a.Lov != 3 * RW * a.N) v = 0;
+    constexpr int P = XW ? 1 : 0;
+    if (v == 1) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, P, 1>;
+    if (v == 3) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, P, 3>;
+    if (v == 5) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, P, 5>;
+    if (v == 7) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, P, 7>;
+    if constexpr (kExperiments && RW == 14 && SPANS && XW && WFLAT) {
+      // timing variants of V 1 (results invalid): 8 no workgroup barriers, 16 no twiddle tables
+      if (v == 9) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, P, 9>;
+      if (v == 17) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, P, 17>;
+      if (v == 25) kern = synth_wave_kernel<RW, SPANS, 10, XW, FIRV, WFLAT, P, 25>;
+    }
+  }
   hipError_t e = set_lds(kern, kLdsB);
   if (e != hipSuccess) return e;
   const int groups = a.N / kCols;

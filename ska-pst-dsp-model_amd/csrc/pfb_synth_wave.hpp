@@ -126,12 +126,34 @@ struct RangeSched {
 // barrier and the swap-1 barrier (1), from the swap-2 barrier to the block's stores (2),
 // from the swap-1 barrier to the swap-2 barrier (4); 8 / 16: as 1 with priority 3 / 1;
 // 32: the loop-top barrier moved below pass 1
+// V (bit mask, round 6):
+//   1  KEPT: with keep = 160 = 16 DK and Ov = 48 the kept outputs are t1 in [3 RW, 13 RW)
+//      (L_ov = 3 RW N), i.e. exactly pass-3 registers t1b in [3, 13) of every lane: only
+//      those 10 are formed (the other 6 of the 16-point IDFT are dead code) and stored, and a
+//      whole block stores them through scalar row offsets from ONE lane offset register that
+//      stays fixed for the kernel.  (Before: 16 stores a block, 6 of them always out of
+//      range, each with its own hoisted address register — 16 VGPRs.)
+//   2  PP: the block loop unrolled by two over two register sets, so block b + 1's rows load
+//      straight into the registers block b + 1 reads.  (Before: one set; pass 1 still held
+//      its registers when the prefetch was issued, so the loads went to temporaries and the
+//      compiler's copies into the loop-carried set, scheduled into pass 2, each waited for its
+//      load — the prefetch's HBM latency exposed half a block after issue.)
+//   8, 16  timing variants (experiments build, results invalid): 8 wave barriers instead of
+//      the block loop's workgroup barriers, 16 a uniform twiddle instead of the LDS tables
+//   4  DEFER (with KEPT, as synth_wave512_kernel): block b's stores are issued at the top of
+//      block b + 1, right after its first barrier, from registers reserved until block b + 1's
+//      pass 3; stores at the end of their own block made the loop latch's copies of the
+//      prefetched rows wait for them (vmcnt counts the stores issued after the loads).
 template <int RW, bool SPANS, int DK, class SCHED, bool XW = false, class FIRV = NoFir, bool WFLAT = false,
-          int PRIO = 0>
+          int PRIO = 0, int V = 0>
 __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol, int tg, const SCHED& sch) {
   constexpr int W = 16 * RW;
+  constexpr bool KEPT = (V & 1) != 0, PP = (V & 2) != 0, DEFER = (V & 4) != 0;
   static_assert(RW <= 14 && RW % 2 == 0, "W = 16 RW with RW even and <= 14");
   static_assert(DK >= 1 && DK <= 16, "keep = 16 DK");
+  static_assert(!KEPT || DK == 10, "KEPT: keep = 160, pass-3 registers [3, 13)");
+  static_assert(!PP || !FIRV::kOn, "PP: stored stage-1 rows only");
+  static_assert(!DEFER || (KEPT && !FIRV::kOn), "DEFER: KEPT stores of stored stage-1 rows");
   static_assert(!FIRV::kOn || !XW, "the FIR synthesis uses the in-wave pass-1 mapping");
   static_assert(!FIRV::kOn || FIRV::rows(0) <= kTilesB / 160, "FIR tile exceeds the phase tiles");
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -269,15 +291,17 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     });
   };
 
-  auto prefetch = [&](int b, auto reuse) {
+  // block b's rows into xd (xd[r] = xs[r + DK] for the reused rows, the others loaded)
+  auto prefetch_into = [&](int b, auto reuse, float2 (&xs)[16], float2 (&xd)[16]) {
     constexpr int R0 = decltype(reuse)::value ? 16 - DK : 0;
-    static_for<0, R0>([&](auto r) { x[r] = x[r + DK]; });
+    static_for<0, R0>([&](auto r) { xd[r] = xs[r + DK]; });
     const __amdgpu_buffer_rsrc_t z = make_rsrc(zpol + (int64_t)b * a.keep * N, zbytes);
     static_for<R0, 16>([&](auto r) {
       const v2u v = __builtin_amdgcn_raw_buffer_load_b64(z, zlane, r * N * 16 * 8, SCHED::kLoadAux);
-      x[r] = __builtin_bit_cast(float2, v);
+      xd[r] = __builtin_bit_cast(float2, v);
     });
   };
+  auto prefetch = [&](int b, auto reuse) { prefetch_into(b, reuse, x, x); };
   [[maybe_unused]] v4u pf[FIRV::kOn ? FIRV::loads(RL) : 1];
   if constexpr (FIRV::kOn) {
     // first block: all 16 register rows from one tile (the phase tiles are not in use yet)
@@ -292,8 +316,40 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
   }
   vm_drain();  // (no store wait at the loop head)
 
-#pragma unroll 1
-  for (int i = 0; i < nb; ++i) {
+  // [[maybe_unused]]: the KEPT full-block store offset of the lane (fixed for the kernel)
+  [[maybe_unused]] const int kept_lane = (t1a < RW) ? (t1a * N + t0g + col2) * 8 : (int)0x80000000;
+  constexpr int TL = KEPT ? 3 : 0, TH = KEPT ? 13 : 16;  // pass-3 registers stored
+  // block b's outputs: y[t - TL] = pass-3 register t of the lane
+  auto store_block = [&](int b, const float2* y) {
+    const int64_t ob = (a.block0 + b) * (int64_t)a.Lkeep;  // first kept output sample
+    const int64_t avail = a.out_limit - ob;
+    const int64_t nk = (tmask(a.timing_mask) & 2)
+                           ? 0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
+    const __amdgpu_buffer_rsrc_t o = make_rsrc(opol + ob, (uint32_t)nk * 8u);
+    if (KEPT && nk == a.Lkeep) {  // uniform: a whole block, every kept output in range
+      // output (t1a + RW t1b) N + t0 - L_ov = lane offset + (t1b - 3) RW N (scalar, >= 0)
+      static_for<TL, TH>([&](auto t) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y[t - TL]), o, (uint32_t)kept_lane,
+                                              (decltype(t)::value - TL) * RW * N * 8, kAuxOut);
+      });
+    } else {
+      // lanes t1a >= RW hold no output: their offsets leave the descriptor's range (as do
+      // the discarded t1 < t1_lo, whose negative offsets wrap past 2^31)
+      int base = (t1a < RW) ? (t1a * N - a.Lov + t0g + col2) * 8 : (int)0x80000000;
+      // (FIR variant: recomputed every block — 16 hoisted store offsets would spill; KEPT: the
+      // ragged last block only)
+      if constexpr (FIRV::kOn || KEPT) asm volatile("" : "+v"(base));
+      // (the whole offset in the lane register: the buffer range check covers the lane
+      // offset, not a scalar offset, and discards the negative t1 < t1_lo offsets)
+      static_for<TL, TH>([&](auto t) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y[t - TL]), o,
+                                              (uint32_t)(base + t * RW * N * 8), 0, kAuxOut);
+      });
+    }
+  };
+  [[maybe_unused]] float2 yprev[TH - TL];  // DEFER: the previous block's outputs
+  // one block: pass 1 reads xc, block i + 1's rows go to xn (xn == xc without PP)
+  auto run_block = [&](int i, float2 (&xc)[16], float2 (&xn)[16]) {
     const int b = sch.block(i);
     // every wave has read the previous block's swap-2 data (from all tiles), and the
     // four waves move through the Z and output lines together
@@ -302,7 +358,10 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     if (wave == 0 && i + 1 < nb) sch.wait(sch.block(i + 1));
     // (PRIO & 32: this barrier moves down to just before the swap-1 writes — pass 1 touches
     // only the constant tables in LDS, so it may overlap other waves' pass 3)
-    if constexpr (!(PRIO & 32)) __syncthreads();
+    if constexpr (!(PRIO & 32)) wave_wg_sync<V>();
+    if constexpr (DEFER) {
+      if (i > 0) store_block(sch.block(i - 1), yprev);  // uniform per workgroup
+    }
     if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(2);
     if constexpr (PRIO & 8) __builtin_amdgcn_s_setprio(3);
     if constexpr (PRIO & 16) __builtin_amdgcn_s_setprio(1);
@@ -313,9 +372,9 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       const v4f q3 = *reinterpret_cast<const v4f*>(winrow + 48);  // r >= 12
       static_for<0, 16>([&](auto rv) {
         constexpr int r = decltype(rv)::value;
-        if constexpr (r < 3) v[r] = cscale(x[r], q0[r]);
-        else if constexpr (r > 12) v[r] = cscale(x[r], q3[r - 12]);
-        else v[r] = x[r];
+        if constexpr (r < 3) v[r] = cscale(xc[r], q0[r]);
+        else if constexpr (r > 12) v[r] = cscale(xc[r], q3[r - 12]);
+        else v[r] = xc[r];
       });
     } else {
       float wv[16];
@@ -326,17 +385,21 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
         wv[4 * k + 2] = q.z;
         wv[4 * k + 3] = q.w;
       });
-      static_for<0, 16>([&](auto r) { v[r] = cscale(x[r], wv[r]); });
+      static_for<0, 16>([&](auto r) { v[r] = cscale(xc[r], wv[r]); });
     }
     // the next block's rows (the last block re-reads itself: the wait count stays fixed)
     if constexpr (FIRV::kOn)
       tile_load(sch.block(min(i + 1, nb - 1)), std::integral_constant<int, RL>{}, pf);
     else
-      prefetch(sch.block(min(i + 1, nb - 1)), std::integral_constant<bool, (SCHED::kReuse && DK < 16)>{});
+      prefetch_into(sch.block(min(i + 1, nb - 1)), std::integral_constant<bool, (SCHED::kReuse && DK < 16)>{}, xc, xn);
     sdft<16, -1>(v);
     {
       float2 w[16];
-      static_for<0, 8>([&](auto k) { lds_pair(tw1row + 16 * k, w[2 * k], w[2 * k + 1]); });
+      if constexpr ((V & 16) != 0) {  // (timing variant: a uniform twiddle, no table reads)
+        static_for<0, 16>([&](auto k) { w[k] = make_float2(a.scale, a.scale); });
+      } else {
+        static_for<0, 8>([&](auto k) { lds_pair(tw1row + 16 * k, w[2 * k], w[2 * k + 1]); });
+      }
       static_for<1, 16>([&](auto f) { v[f] = cmul(v[f], w[f]); });
     }
     if constexpr ((PRIO & 32) != 0) __syncthreads();
@@ -346,7 +409,7 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       *reinterpret_cast<float2*>(lds + wr1 + fr * kRowB) = v[fr];
     });
     if constexpr (PRIO & 25) __builtin_amdgcn_s_setprio(0);
-    if constexpr (XW) __syncthreads();  // the phase tiles were written by every wave
+    if constexpr (XW) wave_wg_sync<V>();  // the phase tiles were written by every wave
     else __builtin_amdgcn_wave_barrier();
     if constexpr (PRIO & 4) __builtin_amdgcn_s_setprio(2);
     static_for<0, 8>([&](auto k) {
@@ -362,7 +425,11 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     sdft<RW, +1>(u);
     {
       float2 w[RW];
-      static_for<0, RW / 2>([&](auto k) { lds_pair(tw2row + 16 * k, w[2 * k], w[2 * k + 1]); });
+      if constexpr ((V & 16) != 0) {
+        static_for<0, RW>([&](auto k) { w[k] = make_float2(a.scale, a.scale); });
+      } else {
+        static_for<0, RW / 2>([&](auto k) { lds_pair(tw2row + 16 * k, w[2 * k], w[2 * k + 1]); });
+      }
       static_for<1, RW>([&](auto t) { u[t] = cmul(u[t], w[t]); });
     }
     // ---- swap 2 (across the workgroup): element (row t1a, slot f1 = l) of this phase's
@@ -373,30 +440,24 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
       *reinterpret_cast<float2*>(lds + wr + tr * kRowB) = u[tr];
     });
     if constexpr (PRIO & 4) __builtin_amdgcn_s_setprio(0);
-    __syncthreads();
+    wave_wg_sync<V>();
     if constexpr (PRIO & 2) __builtin_amdgcn_s_setprio(2);
     static_for<0, 8>([&](auto k) {
       lds_pair(lds + rd2 + 16 * k, v[2 * k], v[2 * k + 1]);
     });
     // ---- pass 3: 16-point IDFT over f1 -> t1 = t1a + RW t1b; overlap-discard on the store
+    // (KEPT: registers t1b outside [3, 13) are never read, so their outputs are not formed)
+    if constexpr (DEFER) {
+      // (the stored registers stay reserved until here — an empty use — so nothing else is
+      // allocated into them while their stores are in flight)
+#pragma unroll
+      for (int t = 0; t < TH - TL; ++t) asm volatile("" ::"v"(yprev[t]));
+    }
     sdft<16, +1>(v);
-    {
-      const int64_t ob = (a.block0 + b) * (int64_t)a.Lkeep;  // first kept output sample
-      const int64_t avail = a.out_limit - ob;
-      const int64_t nk = (tmask(a.timing_mask) & 2)
-                             ? 0 : max((int64_t)0, avail < a.Lkeep ? avail : (int64_t)a.Lkeep);
-      const __amdgpu_buffer_rsrc_t o = make_rsrc(opol + ob, (uint32_t)nk * 8u);
-      // lanes t1a >= RW hold no output: their offsets leave the descriptor's range (as do
-      // the discarded t1 < t1_lo, whose negative offsets wrap past 2^31)
-      int base = (t1a < RW) ? (t1a * N - a.Lov + t0g + col2) * 8 : (int)0x80000000;
-      // (FIR variant: recomputed every block — 16 hoisted store offsets would spill)
-      if constexpr (FIRV::kOn) asm volatile("" : "+v"(base));
-      // (the whole offset in the lane register: the buffer range check covers the lane
-      // offset, not a scalar offset, and discards the negative t1 < t1_lo offsets)
-      static_for<0, 16>([&](auto t) {
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v[t]), o,
-                                              (uint32_t)(base + t * RW * N * 8), 0, kAuxOut);
-      });
+    if constexpr (DEFER) {
+      static_for<TL, TH>([&](auto t) { yprev[t - TL] = v[t]; });
+    } else {
+      store_block(b, v + TL);
     }
     if constexpr (PRIO & 2) __builtin_amdgcn_s_setprio(0);
     if constexpr (FIRV::kOn) {
@@ -413,10 +474,25 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
         fir_rows(std::integral_constant<int, RL>{});
       }
     }
+  };
+  if constexpr (PP) {
+    float2 x2[16];
+    int i = 0;
+#pragma unroll 1
+    for (; i + 1 < nb; i += 2) {
+      run_block(i, x, x2);
+      run_block(i + 1, x2, x);
+    }
+    if (i < nb) run_block(i, x, x2);  // uniform per workgroup
+  } else {
+#pragma unroll 1
+    for (int i = 0; i < nb; ++i) run_block(i, x, x);
   }
+  if constexpr (DEFER) store_block(sch.block(nb - 1), yprev);  // the range's last block
 }
 
-template <int RW, bool SPANS, int DK, bool XW = false, class FIRV = NoFir, bool WFLAT = false, int PRIO = 0>
+template <int RW, bool SPANS, int DK, bool XW = false, class FIRV = NoFir, bool WFLAT = false, int PRIO = 0,
+          int V = 0>
 __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(3)))
 void synth_wave_kernel(SynthBlockArgs a) {
   const int groups = a.N / kCols;
@@ -425,8 +501,8 @@ void synth_wave_kernel(SynthBlockArgs a) {
   const int Rg = gridDim.x / groups;
   const int b_begin = (int)((int64_t)a.n_blocks * rr / Rg);
   const int b_end = (int)((int64_t)a.n_blocks * (rr + 1) / Rg);
-  synth_wave_body<RW, SPANS, DK, RangeSched, XW, FIRV, WFLAT, PRIO>(a, blockIdx.y, lt % groups,
-                                                              RangeSched{b_begin, b_end - b_begin});
+  synth_wave_body<RW, SPANS, DK, RangeSched, XW, FIRV, WFLAT, PRIO, V>(a, blockIdx.y, lt % groups,
+                                                                 RangeSched{b_begin, b_end - b_begin});
 }
 
 }  // namespace pfb

@@ -96,12 +96,17 @@ __device__ __forceinline__ float2 pair_bfly(float2 a, float sg) {
   return make_float2(pair_fma(a.x, sg), pair_fma(a.y, sg));
 }
 
-// v[i] *= row[i], i < 2 NP (one ds_read_b128 per pair, multiplied as it arrives)
-template <int NP>
-__device__ __forceinline__ void twiddle_rows(float2* v, const char* row) {
+// v[i] *= row[i], i < 2 NP (one ds_read_b128 per pair, multiplied as it arrives; TM bit 4,
+// a compile-time timing variant of the experiments build: a uniform value u instead)
+template <int NP, int TM = 0>
+__device__ __forceinline__ void twiddle_rows(float2* v, const char* row, float u = 0.f) {
   static_for<0, NP>([&](auto k) {
     float2 w0, w1;
-    lds_pair2(row + 16 * k, w0, w1);
+    if constexpr ((TM & 16) != 0) {
+      w0 = w1 = make_float2(u, u);
+    } else {
+      lds_pair2(row + 16 * k, w0, w1);
+    }
     v[2 * k] = cmul(v[2 * k], w0);
     v[2 * k + 1] = cmul(v[2 * k + 1], w1);
   });
@@ -144,7 +149,10 @@ __device__ __forceinline__ void idft16_mid8(const float2* v, float2* y) {
 // buffer store wait for that store (vmcnt); with the stores at the end of their own block,
 // the next block's first register writes waited at the loop top for the stores it had just
 // issued (s_waitcnt vmcnt(0) there) — a store round trip per block, exposed.
-template <bool SPANS, bool XW, bool WFLAT = false, int PRIO = 0, bool DEFER = true>
+// TM: compile-time timing variants (experiments build only, results invalid): 8 wave
+// barriers instead of the block loop's workgroup barriers, 16 a uniform twiddle instead of
+// the four LDS twiddle tables
+template <bool SPANS, bool XW, bool WFLAT = false, int PRIO = 0, bool DEFER = true, int TM = 0>
 __global__ __launch_bounds__(kW5Threads) __attribute__((amdgpu_waves_per_eu(3)))
 void synth_wave512_kernel(SynthBlockArgs a) {
   constexpr int W = 448, DK = 8;  // keep = 256 rows = 8 register rows of 32
@@ -289,7 +297,7 @@ void synth_wave512_kernel(SynthBlockArgs a) {
   for (int i = 0; i < nb; ++i) {
     const int b = b_begin + i;
     // every wave has read the previous block's swap-2 data (from all tiles)
-    __syncthreads();
+    wave_wg_sync<TM>();
     if constexpr (DEFER) {
       if (i > 0) store_block(b - 1, yprev);  // uniform per workgroup
     }
@@ -319,19 +327,19 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     // the next block's rows (the last block re-reads itself: the wait count stays fixed)
     prefetch(min(b + 1, b_end - 1), std::true_type{});
     sdft<16, -1>(v);
-    twiddle_rows<8>(v, tw1row);
+    twiddle_rows<8, TM>(v, tw1row, a.scale);
     // ---- swap 1 (inside the wave): A_m[f1] -> tile[f1][m >> 4][m & 15]
     static_for<0, 16>([&](auto f) {
       *reinterpret_cast<float2*>(lds + wr1 + decltype(f)::value * (2 * kRowB)) = v[decltype(f)::value];
     });
     if constexpr (PRIO & 1) __builtin_amdgcn_s_setprio(0);
-    if constexpr (XW) __syncthreads();  // the phase tiles were written by every wave
+    if constexpr (XW) wave_wg_sync<TM>();  // the phase tiles were written by every wave
     else __builtin_amdgcn_wave_barrier();
     static_for<0, 8>([&](auto k) { lds_pair2(lds + rd1 + 16 * k, v[2 * k], v[2 * k + 1]); });
     // ---- pass 2: radix-2 across the lane pair (m = l' + 16 h), x (-)w_32^{g l'},
     // 16-point DFT over l'
     static_for<0, 16>([&](auto l) { v[l] = pair_bfly(v[l], sg); });
-    twiddle_rows<8>(v, tw32row);
+    twiddle_rows<8, TM>(v, tw32row, a.scale);
     sdft<16, -1>(v);
     // ---- kept bins (registers f2'' < 7 and >= 9) x t4, 14-point IDFT over k,
     // x w_28^{g t'}, radix-2 across the pair, x e^{+2 pi i f1 t1a / W}
@@ -344,16 +352,16 @@ void synth_wave512_kernel(SynthBlockArgs a) {
       u[kk] = cmul(v[reg], t4[kk]);
     });
     sdft<14, +1>(u);
-    twiddle_rows<7>(u, w28row);
+    twiddle_rows<7, TM>(u, w28row, a.scale);
     static_for<0, 14>([&](auto t) { u[t] = pair_bfly(u[t], sg); });
-    twiddle_rows<7>(u, tw2row);
+    twiddle_rows<7, TM>(u, tw2row, a.scale);
     // ---- swap 2 (across the workgroup): Y_f1[t1a = t' + 14 e] -> tile[t1a][f1] (the wave's
     // own swap-1 reads of the tile are issued before these writes)
     __builtin_amdgcn_wave_barrier();
     static_for<0, 14>([&](auto t) {
       *reinterpret_cast<float2*>(lds + wr2 + sw2_slot(decltype(t)::value) * kRowB) = u[decltype(t)::value];
     });
-    __syncthreads();
+    wave_wg_sync<TM>();
     static_for<0, 8>([&](auto k) { lds_pair2(lds + rd2 + 16 * k, v[2 * k], v[2 * k + 1]); });
     // ---- pass B: 16-point IDFT over f1 -> t1 = t1a + 28 t1b, only t1b in [4, 12) (the kept
     // outputs: L_ov = 112 N); stored as output sample (t1a + 28 (t1b - 4)) N + t0
@@ -390,6 +398,11 @@ static hipError_t launch_w5(const SynthBlockArgs& a, hipStream_t s) {
     // (PFB_W5_DEFER=0: stores at the end of their own block — experiments build only)
     static const bool nodefer = knob("PFB_W5_DEFER") && std::atoi(knob("PFB_W5_DEFER")) == 0;
     if (nodefer) kern = synth_wave512_kernel<SPANS, XW, WFLAT, 0, false>;
+    // (PFB_W5_TM=8/16/24: the timing variants, results invalid)
+    static const int tm = knob("PFB_W5_TM") ? std::atoi(knob("PFB_W5_TM")) : 0;
+    if (tm == 8) kern = synth_wave512_kernel<SPANS, XW, WFLAT, 0, true, 8>;
+    if (tm == 16) kern = synth_wave512_kernel<SPANS, XW, WFLAT, 0, true, 16>;
+    if (tm == 24) kern = synth_wave512_kernel<SPANS, XW, WFLAT, 0, true, 24>;
   }
   // (PFB_W5_LDS_PAD: extra LDS per workgroup, so fewer workgroups fit a CU — the occupancy
   // slope, experiments build only)
