@@ -7,9 +7,10 @@ set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 EXP=$GRAFT_REPO_ROOT/ska-pst-dsp-model_amd/lib/libpfb_hip_exp.so
+C3V=${VARIANTS:-s:1:0 p:2:0 p:2:6400 p:3:6400 p:2:20000}
 : > gpurun_out/c3pipe.jsonl
 for round in $(seq 1 ${ROUNDS:-1}); do
-for v in ${VARIANTS:-"s:1:0 p:2:0 p:2:6400 p:3:6400 p:2:20000"}; do
+for v in $C3V; do
   IFS=: read mode D pad <<< "$v"
   args="--only-mid --reps ${REPS:-6}"
   if [ "$mode" = p ]; then args="$args --inflight $D --pipeline 1 --graph 1"; fi

@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--n-pol", type=int, default=1)
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="1: the K steps as bench.py's captured two-stream pipeline (capture_pipeline); "
+                         "2: the K steps captured in order on ONE stream as one graph")
     args = ap.parse_args()
     import torch
     import ska_pst_dsp_model_amd as pfb
@@ -65,6 +68,40 @@ def main():
             step()
         torch.cuda.synchronize()
         graphs.append(gr)
+
+    if args.pipeline:
+        # bench.py's timed region: one replay of the K steps as a captured two-stream
+        # pipeline (step i's analysis beside step i-1's synthesis)
+        sys.path.insert(0, REPO)
+        from bench import capture_pipeline
+        pairs = [(k[0], k[1], k[2], k[3]) for k in keep]
+        inputs = [k[4] for k in keep]
+        if args.pipeline == 1:
+            batch = capture_pipeline(torch, dev, pfb, pairs, inputs, n, args.steps)
+        else:
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                for i in range(args.steps):
+                    a_, s_, c_, o_ = pairs[i % D]
+                    pfb.roundtrip(a_, s_, inputs[i % D], chan=c_, out=o_)
+            torch.cuda.synchronize()
+            batch = g1.replay
+        batch()
+        torch.cuda.synchronize()
+
+        def run_pipe():
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            batch()
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) * 1e6 / args.steps
+        ts = [run_pipe() for _ in range(args.reps)]
+        print(json.dumps({"tag": args.tag, "lib": os.path.basename(_lib.LIB_PATH), "inflight": D,
+                          "pipeline": args.pipeline, "n_pol": args.n_pol,
+                          "env": {k: v for k, v in os.environ.items() if k.startswith("PFB_") and k != "PFB_HIP_LIB"},
+                          "us_per_step": round(float(np.median(ts)), 1),
+                          "us_all": [round(t, 1) for t in ts]}), flush=True)
+        return
 
     def run(k):
         torch.cuda.synchronize()
