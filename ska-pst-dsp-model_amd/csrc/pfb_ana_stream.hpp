@@ -252,8 +252,10 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
   }
 }
 
-template <int N, int P, int NU, int DE, int ZOUT, bool LCBF = false, int GS = 0>
-__global__ __launch_bounds__(NT) void analysis_stream_kernel(AnalysisArgs a) {
+// WPE: waves per SIMD the register allocation targets (2: 184 VGPRs for the C2 round trip;
+// 3: <= 168, three 51-KB workgroups per CU)
+template <int N, int P, int NU, int DE, int ZOUT, bool LCBF = false, int GS = 0, int WPE = 2>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void analysis_stream_kernel(AnalysisArgs a) {
   const int w = a.linear ? (int)blockIdx.x : xcd_tile(blockIdx.x, gridDim.x);
   analysis_stream_body<N, P, NU, DE, ZOUT, LCBF, GS>(a, blockIdx.y, w, gridDim.x);
 }

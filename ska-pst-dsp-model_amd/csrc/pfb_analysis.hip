@@ -691,6 +691,20 @@ static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
     if (steps > 0) wgs = std::max(wgs, (n_steps + steps - 1) / steps);
     if (lin >= 0) b.linear = lin;
   }
+  if constexpr (kExperiments && !LCBF) {
+    // (PFB_ANA_WPE=3: the round trip's 2-row-run kernel at 3 waves per SIMD, 3 workgroups
+    // per CU unless PFB_ANA_WG_PER_CU says otherwise — experiments A/B)
+    static const int wpe = knob("PFB_ANA_WPE") ? std::atoi(knob("PFB_ANA_WPE")) : 0;
+    if (wpe == 3 && a.z && a.zblk == 2) {
+      kern = analysis_stream_kernel<N, P, NU, DE, 2, false, 0, 3>;
+      e = set_lds(kern, SH::lds_bytes);
+      if (e != hipSuccess) return e;
+      if (env_wpc <= 0) {
+        const int64_t pp = std::max<int64_t>(1, (3 * cu_count()) / a.n_pol);
+        wgs = std::max(std::min<int64_t>(n_steps, pp), (n_steps + fit_steps - 1) / fit_steps);
+      }
+    }
+  }
   if (wgs > INT32_MAX) return hipErrorInvalidValue;
   dim3 grid((unsigned)wgs, (unsigned)a.n_pol);
   return launch_kernel(kern, grid, dim3(NT), SH::lds_bytes, s, b);

@@ -152,7 +152,12 @@ __device__ __forceinline__ void idft16_mid8(const float2* v, float2* y) {
 // TM: compile-time timing variants (experiments build only, results invalid): 8 wave
 // barriers instead of the block loop's workgroup barriers, 16 a uniform twiddle instead of
 // the four LDS twiddle tables
-template <bool SPANS, bool XW, bool WFLAT = false, int PRIO = 0, bool DEFER = true, int TM = 0>
+// CT (round 6): the two lane-pair twiddles (pass 2's -w_32^{l'} and pass A's w_28^{+t'}) are
+// 1 on lane h = 0 and a compile-time constant per register on lane h = 1, so lane h = 1
+// multiplies by compile-time constants (ctw: quarter turns exact, the others rounded once
+// from double) under an exec mask and lane h = 0 skips them — 15 of the block's 30 twiddle
+// ds_read_b128 gone, no VALU added.  (Before: rows [h][l'] of two LDS tables.)
+template <bool SPANS, bool XW, bool WFLAT = false, int PRIO = 0, bool DEFER = true, int TM = 0, bool CT = true>
 __global__ __launch_bounds__(kW5Threads) __attribute__((amdgpu_waves_per_eu(3)))
 void synth_wave512_kernel(SynthBlockArgs a) {
   constexpr int W = 448, DK = 8;  // keep = 256 rows = 8 register rows of 32
@@ -339,7 +344,12 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     // ---- pass 2: radix-2 across the lane pair (m = l' + 16 h), x (-)w_32^{g l'},
     // 16-point DFT over l'
     static_for<0, 16>([&](auto l) { v[l] = pair_bfly(v[l], sg); });
-    twiddle_rows<8, TM>(v, tw32row, a.scale);
+    if constexpr (CT && !(TM & 16)) {
+      // lane h = 1: x -w_32^{l'} = e^{-2 pi i (l' + 16) / 32}
+      if (h) static_for<0, 16>([&](auto l) { v[l] = ctw<decltype(l)::value + 16, 32, -1>(v[l]); });
+    } else {
+      twiddle_rows<8, TM>(v, tw32row, a.scale);
+    }
     sdft<16, -1>(v);
     // ---- kept bins (registers f2'' < 7 and >= 9) x t4, 14-point IDFT over k,
     // x w_28^{g t'}, radix-2 across the pair, x e^{+2 pi i f1 t1a / W}
@@ -352,7 +362,12 @@ void synth_wave512_kernel(SynthBlockArgs a) {
       u[kk] = cmul(v[reg], t4[kk]);
     });
     sdft<14, +1>(u);
-    twiddle_rows<7, TM>(u, w28row, a.scale);
+    if constexpr (CT && !(TM & 16)) {
+      // lane h = 1: x e^{+2 pi i t' / 28}
+      if (h) static_for<0, 14>([&](auto t) { u[t] = ctw<decltype(t)::value, 28, +1>(u[t]); });
+    } else {
+      twiddle_rows<7, TM>(u, w28row, a.scale);
+    }
     static_for<0, 14>([&](auto t) { u[t] = pair_bfly(u[t], sg); });
     twiddle_rows<7, TM>(u, tw2row, a.scale);
     // ---- swap 2 (across the workgroup): Y_f1[t1a = t' + 14 e] -> tile[t1a][f1] (the wave's
@@ -395,6 +410,9 @@ template <bool SPANS, bool XW, bool WFLAT = false>
 static hipError_t launch_w5(const SynthBlockArgs& a, hipStream_t s) {
   auto kern = synth_wave512_kernel<SPANS, XW, WFLAT>;
   if constexpr (kExperiments && XW && WFLAT) {
+    // (PFB_W5_CT=0: the lane-pair twiddles from the LDS tables — experiments build only)
+    static const bool noct = knob("PFB_W5_CT") && std::atoi(knob("PFB_W5_CT")) == 0;
+    if (noct) kern = synth_wave512_kernel<SPANS, XW, WFLAT, 0, true, 0, false>;
     // (PFB_W5_DEFER=0: stores at the end of their own block — experiments build only)
     static const bool nodefer = knob("PFB_W5_DEFER") && std::atoi(knob("PFB_W5_DEFER")) == 0;
     if (nodefer) kern = synth_wave512_kernel<SPANS, XW, WFLAT, 0, false>;
