@@ -576,6 +576,25 @@ def capture_step(torch, dev, fn):
     return graph.replay
 
 
+def capture_chain(torch, dev, fns):
+    """The calls ``fns`` one after another on one stream, captured as ONE graph (after an
+    eager run of each on a side stream): a replay runs them back to back with no graph-launch
+    gap between them (a per-step replay leaves ~15 us between steps: the C3 kernel trace,
+    profiles/r06_v13_c3_step_trace.json).  Returns the graph's replay."""
+    graph = torch.cuda.CUDAGraph()
+    cs = torch.cuda.Stream(device=dev)
+    cs.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(cs):
+        for fn in fns:
+            fn()
+    torch.cuda.current_stream(dev).wait_stream(cs)
+    with torch.cuda.graph(graph):
+        for fn in fns:
+            fn()
+    torch.cuda.synchronize(dev)
+    return graph.replay
+
+
 def measure_c3(args, torch, dist, world, dev, pfb, lib, c3):
     """BASELINE configs[2]: SKA-Mid padded round trip — 4096 channels, OS
     8/7, 100 353 two-stage firls taps, 2^26 samples, Nf 512, Ov 128, tukey, deripple —
@@ -609,17 +628,21 @@ def measure_c3(args, torch, dist, world, dev, pfb, lib, c3):
         steps[i % D]()
     torch.cuda.synchronize(dev)
     sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
-    # timed region (`ms`): the K steps one at a time, one graph replay per step on one stream,
-    # the pairs' units in turn.  The captured two-stream pipeline of the C2 headline
-    # (`ms_pipelined`, D > 1) measured SLOWER for C3 (0.862 vs 0.810 ms, r06_v4): its FIR
-    # beside the Nf 512 synthesis contends for the CUs that kernel is bound by.
+    # timed region (`ms`): the K steps, step i on pair i mod D (its own unit), one after
+    # another on one stream, captured as ONE graph: no graph-launch gap between steps.  The
+    # captured two-stream pipeline of the C2 headline (`ms_pipelined`, D > 1) measured SLOWER
+    # for C3 (0.862 vs 0.810 ms, r06_v4): its FIR beside the Nf 512 synthesis contends for the
+    # CUs that kernel is bound by.  `ms_per_replay`: one graph replay per step (round 6 before
+    # the chain: ~15 us of launch gap per step in the kernel trace, r06_v13_c3_step_trace.json).
+    chain = capture_chain(torch, dev, [steps[i % D] for i in range(args.steps)])
+    el = timed_region(1, chain, world, dist, sync)
     ones = [capture_step(torch, dev, st) for st in steps]
     ctr = [0]
 
     def one():
         ones[ctr[0] % D]()
         ctr[0] += 1
-    el = timed_region(args.steps, one, world, dist, sync)
+    el_replay = timed_region(args.steps, one, world, dist, sync)
     el_pipe = None
     if D > 1 and args.pipeline:
         batch = capture_pipeline(torch, dev, pfb, pairs, inputs, C3_N_DAT, args.steps)
@@ -639,8 +662,9 @@ def measure_c3(args, torch, dist, world, dev, pfb, lib, c3):
                        "samples, Nf 512, Ov 128, tukey, deripple; 1 single-pol unit per step" % len(taps),
            "ms": round(ms, 4), "value": round(C3_N_DAT / (ms * 1e-3) / 1e6, 2),
            "unit": "complex Msamples/s", "steps": args.steps,
+           "ms_per_replay": round(el_replay / args.steps * 1e3, 4),
            "ms_pipelined": round(el_pipe / args.steps * 1e3, 4) if el_pipe else None,
-           "plan_pairs": D, "pipeline": False, "hip_graph": True,
+           "plan_pairs": D, "pipeline": False, "hip_graph": "one graph of the K steps on one stream",
            "unit_seeds": [300 + 7919 * p for p in range(D)],
            "channelised_rows": K, "output_samples": n_out,
            "roofline": {"bound": "hbm", "alg_bytes_per_step": b_alg, "achieved": round(gbs, 1),
@@ -664,13 +688,19 @@ def measure_synthesis_only(args, torch, dist, world, dev, pfb, lib, ana, taps, x
     syn = pfb.SynthesisPlan(N_CHAN, OS_STR, NF, OV, True, 1, True, taps, win, None, chan.shape[0], dev.index or 0)
     K = chan.shape[1]
     n_out = syn.output_length(K)
+    obuf = torch.empty((chan.shape[0], n_out), dtype=torch.complex64, device=dev)
 
     def step():
-        syn.execute(chan, layout="ptc")
+        syn.execute(chan, layout="ptc", out=obuf)
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize(dev)
-    el = timed_region(args.steps, step, world, dist, lambda: torch.cuda.synchronize(dev))
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+    # timed region: the K calls captured as one graph (no host launch gaps between the
+    # calls' kernels); `ms_eager`: the K calls launched from Python one by one
+    chain = capture_chain(torch, dev, [step] * args.steps)
+    el = timed_region(1, chain, world, dist, sync)
+    el_eager = timed_region(args.steps, step, world, dist, sync)
     lib.pfb_profile_reset()
     lib.pfb_profile_enable(1)
     timed_region(args.steps, step, world, dist, lambda: torch.cuda.synchronize(dev))
@@ -685,10 +715,11 @@ def measure_synthesis_only(args, torch, dist, world, dev, pfb, lib, ana, taps, x
                        "%d output samples per pol (Nf 256, Ov 48, tukey, deripple)" % (K, n_out),
            "ms": round(ms, 4), "value": round(n_pol * n_out / (ms * 1e-3) / 1e6, 2),
            "unit": "complex Msamples/s (output samples)", "steps": args.steps,
+           "ms_eager": round(el_eager / args.steps * 1e3, 4), "hip_graph": "one graph of the K calls",
            "roofline": {"bound": "hbm", "alg_bytes_per_step": b_alg, "achieved": round(gbs, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)},
            "kernels": kern}
-    del chan
+    del chan, obuf
     syn.close()
     return res
 

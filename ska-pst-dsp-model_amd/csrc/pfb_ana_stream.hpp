@@ -59,14 +59,30 @@ struct ColMajorLds {
   __device__ __forceinline__ float2 load(int row, int c) const { return b[c * (T + 1) + row]; }
 };
 
+// timing variant TV 16: a store functor that only keeps the value live (no instruction)
+struct SinkStore {
+  static constexpr bool kIsLds = false;
+  __device__ __forceinline__ void store(int, int, float2 v) const { asm volatile("" ::"v"(v)); }
+};
+
 // ZOUT: 0 no stage-1 rows; 1 rows [row][c] (AnalysisArgs::z); 2 / 4: runs of ZOUT rows per
 // column (AnalysisArgs::zblk) for the synthesis wave kernel.
 // Streaming analysis of step range w of nw (steps of T rows from row0) for polarisation
 // pol.
-template <int N, int P, int NU, int DE, int ZOUT, bool LCBF, int GS>
+// TV: compile-time timing variants (experiments build only, results invalid): 1 no FIR (one
+// window row per output row instead of the PE-tap sums), 2 no FFT (no channelised rows), 4 no
+// window slide (the prefetched rows are not moved into the window), 16 the FFT without its
+// channelised-row stores; 8 (valid, the A/B of
+// round 6): workgroup barriers inside the FFT (the pre-round-6 form)
+// The step's N-point FFT: thread c's butterfly of both radix-16 passes lies in row c / 16, so
+// wave w owns rows 4w .. 4w + 3 for the whole transform (wave_rows_ok) and the two barriers
+// inside it are wave barriers (round 6; timing variants r06_v14: the FFT was 30 of the
+// kernel's 78 us with four workgroup barriers a step, memory traffic masked or not)
+template <int N, int P, int NU, int DE, int ZOUT, bool LCBF, int GS, int TV = 0>
 __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int pol, int w, int nw) {
   using SH = StreamShape<N, P, NU, DE>;
   constexpr int M = SH::M, PE = SH::PE, QS = SH::QS, T = SH::T, NEW = SH::NEW, WIN = SH::WIN;
+  constexpr bool kWR = (TV & 8) == 0 && wave_rows_ok<N, T, NT>();
   extern __shared__ __attribute__((aligned(16))) float2 smem[];
   const int c = threadIdx.x;
   if constexpr (ZOUT == 0 && !LCBF) {  // (stream objects only: no round-trip / LowCBF kernel)
@@ -158,6 +174,13 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
 #pragma unroll
       for (int qq = 0; qq < QS; ++qq) acc[decltype(sv)::value][qq] = v2f{0.f, 0.f};
     });
+    if constexpr ((TV & 1) != 0) {
+      static_for<0, NU>([&](auto sv) {
+        static_for<0, QS>([&](auto qv) {
+          acc[decltype(sv)::value][decltype(qv)::value] = win[DE * decltype(qv)::value + decltype(sv)::value];
+        });
+      });
+    } else
     static_for<0, PE>([&](auto mv) {
       constexpr int m = decltype(mv)::value;
       float gm[NU];
@@ -207,9 +230,10 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
       });
     });
     __syncthreads();
-    if constexpr (LCBF) {
+    if constexpr ((TV & 2) != 0) {
+    } else if constexpr (LCBF) {
       const LcbfRowStore st = LcbfRowStore::rows(opol, k0, T, a.row0, a.K, a.lcbf_scale);
-      block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
+      block_fft<N, -1, T, NT, kWR>(rows, st, rows, tw, c);
     } else if constexpr (GS == 2) {
       // channel-major (a cascade's stage-2 series, out_rs = 1, no chomp): the last pass
       // lands in LDS by channel, then each 8-lane group writes one channel's T = 16
@@ -222,7 +246,7 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
       // store count per step.)
       static_assert(N * (T + 1) <= T * SH::RS, "channel-major staging exceeds the LDS rows");
       const ColMajorLds<T> cm{smem};
-      block_fft<N, -1, T, NT>(rows, cm, rows, tw, c);
+      block_fft<N, -1, T, NT, kWR>(rows, cm, rows, tw, c);
       __syncthreads();
       const int hi = (int)min(max(a.K - k0, (int64_t)0), (int64_t)T);
       const int lo = (int)min(max(a.row0 - k0, (int64_t)0), (int64_t)T);
@@ -239,25 +263,34 @@ __device__ __forceinline__ void analysis_stream_body(const AnalysisArgs& a, int 
     } else if constexpr (GS == 1) {
       const StridedRowStore st = StridedRowStore::rows(opol, k0, T, a.row0, a.K, a.out_rs, a.out_cs,
                                                        a.sel_split, a.sel_shift, a.sel_n, N, (float)N);
-      block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
+      block_fft<N, -1, T, NT, kWR>(rows, st, rows, tw, c);
+    } else if constexpr ((TV & 16) != 0) {
+      // (timing variant: the FFT computed, its channelised rows not stored — kept live only)
+      block_fft<N, -1, T, NT, kWR>(rows, SinkStore{}, rows, tw, c);
     } else {
       // (timing mask bit 1, experiments build: no channelised stores)
       const BufRowStore st = BufRowStore::rows(opol, k0, T, a.row0, (tmask(a.timing_mask) & 2) ? k0 : a.K, N, (float)N);
-      block_fft<N, -1, T, NT>(rows, st, rows, tw, c);
+      block_fft<N, -1, T, NT, kWR>(rows, st, rows, tw, c);
     }
+    if constexpr ((TV & 4) != 0) {
+      // (keep the prefetched rows live: an empty use)
+#pragma unroll
+      for (int i = 0; i < NEW; ++i) asm volatile("" ::"v"(pf[i]));
+    } else {
 #pragma unroll
     for (int i = 0; i < PE - 1; ++i) win[i] = win[i + NEW];
 #pragma unroll
     for (int i = 0; i < NEW; ++i) win[PE - 1 + i] = pf[i];
+    }
   }
 }
 
 // WPE: waves per SIMD the register allocation targets (2: 184 VGPRs for the C2 round trip;
 // 3: <= 168, three 51-KB workgroups per CU)
-template <int N, int P, int NU, int DE, int ZOUT, bool LCBF = false, int GS = 0, int WPE = 2>
+template <int N, int P, int NU, int DE, int ZOUT, bool LCBF = false, int GS = 0, int WPE = 2, int TV = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void analysis_stream_kernel(AnalysisArgs a) {
   const int w = a.linear ? (int)blockIdx.x : xcd_tile(blockIdx.x, gridDim.x);
-  analysis_stream_body<N, P, NU, DE, ZOUT, LCBF, GS>(a, blockIdx.y, w, gridDim.x);
+  analysis_stream_body<N, P, NU, DE, ZOUT, LCBF, GS, TV>(a, blockIdx.y, w, gridDim.x);
 }
 
 }  // namespace pfb

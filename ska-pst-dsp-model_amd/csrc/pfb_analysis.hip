@@ -695,6 +695,28 @@ static hipError_t launch_stream(const AnalysisArgs& a, hipStream_t s) {
     // (PFB_ANA_WPE=3: the round trip's 2-row-run kernel at 3 waves per SIMD, 3 workgroups
     // per CU unless PFB_ANA_WG_PER_CU says otherwise — experiments A/B)
     static const int wpe = knob("PFB_ANA_WPE") ? std::atoi(knob("PFB_ANA_WPE")) : 0;
+    // (PFB_ANA_TV=1..7: the timing variants of the round trip's kernel, results invalid; 8: the
+    // FFT with workgroup barriers, the pre-round-6 kernel)
+    static const int tv = knob("PFB_ANA_TV") ? std::atoi(knob("PFB_ANA_TV")) : 0;
+    if (a.z && a.zblk == 2 && (tv == 8 || tv == 16)) {
+      kern = tv == 8 ? analysis_stream_kernel<N, P, NU, DE, 2, false, 0, 2, 8>
+                     : analysis_stream_kernel<N, P, NU, DE, 2, false, 0, 2, 16>;
+      e = set_lds(kern, SH::lds_bytes);
+      if (e != hipSuccess) return e;
+    }
+    if (a.z && a.zblk == 2 && tv > 0 && tv < 8) {
+      switch (tv) {
+        case 1: kern = analysis_stream_kernel<N, P, NU, DE, 2, false, 0, 2, 1>; break;
+        case 2: kern = analysis_stream_kernel<N, P, NU, DE, 2, false, 0, 2, 2>; break;
+        case 3: kern = analysis_stream_kernel<N, P, NU, DE, 2, false, 0, 2, 3>; break;
+        case 4: kern = analysis_stream_kernel<N, P, NU, DE, 2, false, 0, 2, 4>; break;
+        case 5: kern = analysis_stream_kernel<N, P, NU, DE, 2, false, 0, 2, 5>; break;
+        case 6: kern = analysis_stream_kernel<N, P, NU, DE, 2, false, 0, 2, 6>; break;
+        default: kern = analysis_stream_kernel<N, P, NU, DE, 2, false, 0, 2, 7>; break;
+      }
+      e = set_lds(kern, SH::lds_bytes);
+      if (e != hipSuccess) return e;
+    }
     if (wpe == 3 && a.z && a.zblk == 2) {
       kern = analysis_stream_kernel<N, P, NU, DE, 2, false, 0, 3>;
       e = set_lds(kern, SH::lds_bytes);

@@ -330,7 +330,7 @@ template <int N, int DIR, class Last, class TW, int R0, int... Rest>
 __device__ __forceinline__ void run_rest(const LdsRows& lds, const Last& last, const TW& tw, int tid,
                                          Radices<R0, Rest...>) {
   static_assert(sizeof...(Rest) > 0, "transform has a single pass");
-  run_passes_impl<N, DIR, 1, NT, R0, Rest...>(lds, last, lds, tw, tid);
+  run_passes_impl<N, DIR, 1, NT, false, R0, Rest...>(lds, last, lds, tw, tid);
 }
 
 // Persistent row FFT for one-row-per-workgroup sizes (N >= 4096 with radix-16 first

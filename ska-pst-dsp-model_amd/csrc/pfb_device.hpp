@@ -331,7 +331,11 @@ __device__ __forceinline__ void twiddle_powers(const TW& tw, int m, float2 (&w)[
 // stores through `out`.  All NT threads participate; the pass contains one barrier
 // between its loads and its stores, so `in` and `out` may alias (in-place via
 // registers).  The caller places a barrier before the next pass reads `out`.
-template <int N, int R, int NS, int DIR, int ROWS, int NT, class In, class Out, class TW>
+struct LdsRows;
+// WR (wave rows): every row's butterflies of every pass belong to one wave (wave_rows_ok), so
+// an in-place pass over the LDS rows needs only a wave barrier (a wave's LDS instructions
+// execute in order) — no workgroup barrier between its loads and stores
+template <int N, int R, int NS, int DIR, int ROWS, int NT, bool WR = false, class In, class Out, class TW>
 __device__ __forceinline__ void stockham_pass(const In& in, const Out& out, const TW& tw, int tid) {
   constexpr int NB = N / R;
   constexpr int TOT = ROWS * NB;
@@ -344,7 +348,10 @@ __device__ __forceinline__ void stockham_pass(const In& in, const Out& out, cons
       static_for<0, R>([&](auto r) { v[p][r] = in.load(row, j + r * NB); });
     }
   });
-  if constexpr (In::kIsLds && Out::kIsLds) __syncthreads();
+  if constexpr (In::kIsLds && Out::kIsLds) {
+    if constexpr (WR && std::is_same_v<In, LdsRows> && std::is_same_v<Out, LdsRows>) __builtin_amdgcn_wave_barrier();
+    else __syncthreads();
+  }
   static_for<0, PER>([&](auto p) {
     const int b = tid + p * NT;
     if (TOT % NT == 0 || b < TOT) {
@@ -370,29 +377,44 @@ struct LdsRows : LdsIO {
 };
 
 // Run all passes of FFTPlan<N>; first pass loads via `first`, last pass stores via
-// `last`, intermediate passes go through the LDS rows `lds`.
-template <int N, int DIR, int ROWS, int NT, int NS, int R, int... Rest, class First, class Last, class TW>
+// `last`, intermediate passes go through the LDS rows `lds`.  WR: see stockham_pass (the
+// barrier between two passes is then a wave barrier too).
+template <int N, int DIR, int ROWS, int NT, bool WR, int NS, int R, int... Rest, class First, class Last, class TW>
 __device__ __forceinline__ void run_passes_impl(const First& first, const Last& last,
                                                 const LdsRows& lds, const TW& tw, int tid) {
   if constexpr (sizeof...(Rest) == 0) {
-    stockham_pass<N, R, NS, DIR, ROWS, NT>(first, last, tw, tid);
+    stockham_pass<N, R, NS, DIR, ROWS, NT, WR>(first, last, tw, tid);
   } else {
-    stockham_pass<N, R, NS, DIR, ROWS, NT>(first, lds, tw, tid);
-    __syncthreads();
-    run_passes_impl<N, DIR, ROWS, NT, NS * R, Rest...>(lds, last, lds, tw, tid);
+    stockham_pass<N, R, NS, DIR, ROWS, NT, WR>(first, lds, tw, tid);
+    if constexpr (WR) __builtin_amdgcn_wave_barrier();
+    else __syncthreads();
+    run_passes_impl<N, DIR, ROWS, NT, WR, NS * R, Rest...>(lds, last, lds, tw, tid);
   }
 }
 
-template <int N, int DIR, int ROWS, int NT, class First, class Last, int... Rs>
+template <int N, int DIR, int ROWS, int NT, bool WR = false, class First, class Last, int... Rs>
 __device__ __forceinline__ void run_fft(const First& first, const Last& last, const LdsRows& lds,
                                         const float2* tw, int tid, Radices<Rs...>) {
-  run_passes_impl<N, DIR, ROWS, NT, 1, Rs...>(first, last, lds, tw, tid);
+  run_passes_impl<N, DIR, ROWS, NT, WR, 1, Rs...>(first, last, lds, tw, tid);
 }
 
-template <int N, int DIR, int ROWS, int NT, class First, class Last>
+// Whether every pass of FFTPlan<N> over ROWS rows with NT threads gives each thread one
+// butterfly (PER = 1) and keeps each row's butterflies inside one 64-lane wave: row = tid /
+// (N / R) for every radix R, with N / R dividing 64.
+template <int N, int ROWS, int NT, int... Rs>
+constexpr bool wave_rows_ok_impl(Radices<Rs...>) {
+  return ((ROWS * (N / Rs) == NT && 64 % (N / Rs) == 0) && ...);
+}
+template <int N, int ROWS, int NT>
+constexpr bool wave_rows_ok() { return wave_rows_ok_impl<N, ROWS, NT>(typename FFTPlan<N>::type{}); }
+
+// WR (round 6): wave-owned rows (wave_rows_ok), the passes ordered by wave barriers; the
+// arithmetic is the same, so the output is bit-identical to the workgroup-barrier form
+template <int N, int DIR, int ROWS, int NT, bool WR = false, class First, class Last>
 __device__ __forceinline__ void block_fft(const First& first, const Last& last, const LdsRows& lds,
                                           const float2* tw, int tid) {
-  run_fft<N, DIR, ROWS, NT>(first, last, lds, tw, tid, typename FFTPlan<N>::type{});
+  static_assert(!WR || wave_rows_ok<N, ROWS, NT>(), "WR: a row's butterflies must stay in one wave");
+  run_fft<N, DIR, ROWS, NT, WR>(first, last, lds, tw, tid, typename FFTPlan<N>::type{});
 }
 
 

@@ -348,6 +348,13 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     }
   };
   [[maybe_unused]] float2 yprev[TH - TL];  // DEFER: the previous block's outputs
+  // WFLAT: the lane's window values that are not exactly 1 (rows l + 16 r, r < 3 and r > 12),
+  // held in registers for the whole launch (round 6: 2 LDS reads a block fewer)
+  [[maybe_unused]] v4f wq0{}, wq3{};
+  if constexpr (WFLAT) {
+    wq0 = *reinterpret_cast<const v4f*>(winrow);
+    wq3 = *reinterpret_cast<const v4f*>(winrow + 48);
+  }
   // one block: pass 1 reads xc, block i + 1's rows go to xn (xn == xc without PP)
   auto run_block = [&](int i, float2 (&xc)[16], float2 (&xn)[16]) {
     const int b = sch.block(i);
@@ -368,12 +375,10 @@ __device__ __forceinline__ void synth_wave_body(const SynthBlockArgs& a, int pol
     // ---- pass 1: taper, 16-point DFT over r, twiddle
     float2 v[16];
     if constexpr (WFLAT) {
-      const v4f q0 = *reinterpret_cast<const v4f*>(winrow);       // rows l + 16 r, r < 4
-      const v4f q3 = *reinterpret_cast<const v4f*>(winrow + 48);  // r >= 12
       static_for<0, 16>([&](auto rv) {
         constexpr int r = decltype(rv)::value;
-        if constexpr (r < 3) v[r] = cscale(xc[r], q0[r]);
-        else if constexpr (r > 12) v[r] = cscale(xc[r], q3[r - 12]);
+        if constexpr (r < 3) v[r] = cscale(xc[r], wq0[r]);
+        else if constexpr (r > 12) v[r] = cscale(xc[r], wq3[r - 12]);
         else v[r] = xc[r];
       });
     } else {

@@ -297,6 +297,13 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     }
   };
   [[maybe_unused]] float2 yprev[8];
+  // WFLAT: the lane's 8 window values that are not exactly 1 (rows m + 32 r, r < 4 and
+  // r >= 12), held in registers for the whole launch (round 6: 2 LDS reads a block fewer)
+  [[maybe_unused]] v4f wq0{}, wq3{};
+  if constexpr (WFLAT) {
+    wq0 = *reinterpret_cast<const v4f*>(winrow);
+    wq3 = *reinterpret_cast<const v4f*>(winrow + 48);
+  }
 
 #pragma unroll 1
   for (int i = 0; i < nb; ++i) {
@@ -310,12 +317,10 @@ void synth_wave512_kernel(SynthBlockArgs a) {
     // ---- pass 1: taper, 16-point DFT over r, x w_512^{m f1}
     float2 v[16];
     if constexpr (WFLAT) {
-      const v4f q0 = *reinterpret_cast<const v4f*>(winrow);       // r < 4
-      const v4f q3 = *reinterpret_cast<const v4f*>(winrow + 48);  // r >= 12
       static_for<0, 16>([&](auto rv) {
         constexpr int r = decltype(rv)::value;
-        if constexpr (r < 4) v[r] = cscale(x[r], q0[r]);
-        else if constexpr (r >= 12) v[r] = cscale(x[r], q3[r - 12]);
+        if constexpr (r < 4) v[r] = cscale(x[r], wq0[r]);            // r < 4
+        else if constexpr (r >= 12) v[r] = cscale(x[r], wq3[r - 12]);  // r >= 12
         else v[r] = x[r];
       });
     } else {

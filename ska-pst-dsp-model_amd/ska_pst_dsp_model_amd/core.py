@@ -365,8 +365,10 @@ class SynthesisPlan:
         ptc = x.transpose(0, 2, 1) if layout == "pfc" else x
         return np.ascontiguousarray(ptc, dtype=np.complex64), False
 
-    def execute(self, x, sample_offset: int = 1, stateful: bool = False, layout: str = "pfc"):
-        """Run the synthesis; returns the (n_pol, n_out) series."""
+    def execute(self, x, sample_offset: int = 1, stateful: bool = False, layout: str = "pfc", out=None):
+        """Run the synthesis; returns the (n_pol, n_out) series.  ``out``: an optional
+        contiguous complex64 device buffer of at least (n_pol, output length) samples to
+        write into (device input only; for graph capture without per-call allocations)."""
         ptc, dev = self._prep_in(x, layout)
         if ptc.shape[0] != self.n_pol or ptc.shape[2] != self.n_chan:
             raise ValueError(f"plan built for (n_pol={self.n_pol}, n_chan={self.n_chan}), "
@@ -376,9 +378,17 @@ class SynthesisPlan:
             cap = self.output_length(self.buffered_samples + n_dat)
         else:
             cap = self.output_length(max(n_dat - (int(sample_offset) - 1), 0))
+        if out is not None and not dev:
+            raise ValueError("out= needs device input")
         if dev:
             t = _torch()
-            out = t.empty((self.n_pol, max(cap, 0)), dtype=t.complex64, device=ptc.device)
+            if out is None:
+                out = t.empty((self.n_pol, max(cap, 0)), dtype=t.complex64, device=ptc.device)
+            elif (out.dtype != t.complex64 or out.device != ptc.device or not out.is_contiguous()
+                  or out.dim() != 2 or out.shape[0] != self.n_pol or out.shape[1] < max(cap, 0)):
+                raise ValueError(f"out must be a contiguous complex64 ({self.n_pol}, >= {max(cap, 0)}) "
+                                 f"tensor on {ptc.device}, got {tuple(out.shape)} {out.dtype} {out.device}")
+            cap = out.shape[1] if cap > 0 else cap
             src, dst, mem, stream = c_void_p(ptc.data_ptr()), c_void_p(out.data_ptr()), \
                 _lib.PFB_MEM_DEVICE, _stream_of(ptc, self)
         else:

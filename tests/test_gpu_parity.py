@@ -235,6 +235,30 @@ def test_synthesis_sample_offset(gpu):
     assert_pfb_close(got, ref)
 
 
+def test_synthesis_execute_into_out_buffer(gpu):
+    """SynthesisPlan.execute(..., out=buf) (the bench's graph-captured synthesis-only leg)
+    writes the same samples as the allocating call, bit for bit, into a wider buffer's
+    rows; a buffer too short is refused before any launch."""
+    import torch
+    pfb = _pfb()
+    taps = _taps("low87")
+    N, nf, ov = 256, 256, 48
+    x = _noise(np.random.default_rng(31), (2, 6 * 160 + 2 * ov + 3, N)).astype(np.complex64)
+    win = pfb.PFBWindow().lookup["tukey"](nf, ov)
+    syn = pfb.SynthesisPlan(N, "8/7", nf, ov, True, 1, True, taps, win, None, 2, 0)
+    chan = torch.from_numpy(x).cuda()
+    ref = syn.execute(chan, layout="ptc").cpu().numpy()
+    buf = torch.full((2, ref.shape[1] + 5), complex(7.0, -7.0), dtype=torch.complex64, device="cuda")
+    got = syn.execute(chan, layout="ptc", out=buf)
+    torch.cuda.synchronize()
+    assert got.data_ptr() == buf.data_ptr()
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+    assert (buf[:, ref.shape[1]:].cpu().numpy() == np.complex64(7 - 7j)).all()
+    with pytest.raises(ValueError):
+        syn.execute(chan, layout="ptc", out=buf[:, : ref.shape[1] - 1].contiguous())
+    syn.close()
+
+
 @pytest.mark.parametrize("N,os_,nf,ov,blocks", [
     (256, "8/7", 256, 48, 12),
     (256, "4/3", 256, 48, 10),
