@@ -72,7 +72,8 @@ struct SinkStore {
 // TV: compile-time timing variants (experiments build only, results invalid): 1 no FIR (one
 // window row per output row instead of the PE-tap sums), 2 no FFT (no channelised rows), 4 no
 // window slide (the prefetched rows are not moved into the window), 16 the FFT without its
-// channelised-row stores; 8 (valid, the A/B of
+// channelised-row stores (17 of the kernel's 80 us, r06_v16; written instead as whole 1-KB
+// runs from the wave-owned LDS rows they took 2 us MORE, r06_v17 — rejected); 8 (valid, the A/B of
 // round 6): workgroup barriers inside the FFT (the pre-round-6 form)
 // The step's N-point FFT: thread c's butterfly of both radix-16 passes lies in row c / 16, so
 // wave w owns rows 4w .. 4w + 3 for the whole transform (wave_rows_ok) and the two barriers
