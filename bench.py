@@ -595,12 +595,14 @@ def capture_chain(torch, dev, fns):
     return graph.replay
 
 
-def measure_c3(args, torch, dist, world, dev, pfb, lib, c3):
+def measure_c3(args, torch, dist, world, dev, pfb, lib, c3, n_pol=1):
     """BASELINE configs[2]: SKA-Mid padded round trip — 4096 channels, OS
     8/7, 100 353 two-stage firls taps, 2^26 samples, Nf 512, Ov 128, tukey, deripple —
     through pfb_roundtrip_execute (FIR -> row FFT -> synthesis), input resident in HBM.
     K timed steps between barrier + synchronize, then the same K with HIP events around
-    every kernel (per-kernel durations and the roofline)."""
+    every kernel (per-kernel durations and the roofline).  n_pol = 2: the SKA-Mid `mid`
+    sub-config's dual-polarisation unit (config/test.config.json:104-128), one launch per
+    kernel for both pols (the `dual_pol` key; the per-replay and pipelined regions skipped)."""
     taps = c3["taps"]
     win = pfb.PFBWindow().lookup["tukey"](C3_NF, C3_OV)
     D = max(1, args.inflight)
@@ -609,16 +611,16 @@ def measure_c3(args, torch, dist, world, dev, pfb, lib, c3):
     pairs, inputs = [], []
     for p in range(D):
         g = torch.Generator(device=dev).manual_seed(300 + 7919 * p)
-        inputs.append((torch.complex(torch.randn((1, C3_N_DAT), device=dev, generator=g),
-                                     torch.randn((1, C3_N_DAT), device=dev, generator=g)) /
+        inputs.append((torch.complex(torch.randn((n_pol, C3_N_DAT), device=dev, generator=g),
+                                     torch.randn((n_pol, C3_N_DAT), device=dev, generator=g)) /
                        np.sqrt(2.0)).to(torch.complex64))
-        ana = pfb.AnalysisPlan(taps, C3_N_CHAN, OS_STR, "polyphase_analysis_padded", 1, dev.index or 0)
-        syn = pfb.SynthesisPlan(C3_N_CHAN, OS_STR, C3_NF, C3_OV, True, 1, True, taps, win, None, 1,
+        ana = pfb.AnalysisPlan(taps, C3_N_CHAN, OS_STR, "polyphase_analysis_padded", n_pol, dev.index or 0)
+        syn = pfb.SynthesisPlan(C3_N_CHAN, OS_STR, C3_NF, C3_OV, True, 1, True, taps, win, None, n_pol,
                                 dev.index or 0)
         K = ana.output_length(C3_N_DAT)
         n_out = syn.output_length(K)
-        pairs.append((ana, syn, torch.empty((1, K, C3_N_CHAN), dtype=torch.complex64, device=dev),
-                      torch.empty((1, n_out), dtype=torch.complex64, device=dev)))
+        pairs.append((ana, syn, torch.empty((n_pol, K, C3_N_CHAN), dtype=torch.complex64, device=dev),
+                      torch.empty((n_pol, n_out), dtype=torch.complex64, device=dev)))
 
     def step_of(p):
         ana, syn, chan, out = pairs[p]
@@ -636,15 +638,17 @@ def measure_c3(args, torch, dist, world, dev, pfb, lib, c3):
     # the chain: ~15 us of launch gap per step in the kernel trace, r06_v13_c3_step_trace.json).
     chain = capture_chain(torch, dev, [steps[i % D] for i in range(args.steps)])
     el = timed_region(1, chain, world, dist, sync)
-    ones = [capture_step(torch, dev, st) for st in steps]
-    ctr = [0]
+    del chain
+    el_replay = el_pipe = None
+    if n_pol == 1:
+        ones = [capture_step(torch, dev, st) for st in steps]
+        ctr = [0]
 
-    def one():
-        ones[ctr[0] % D]()
-        ctr[0] += 1
-    el_replay = timed_region(args.steps, one, world, dist, sync)
-    el_pipe = None
-    if D > 1 and args.pipeline:
+        def one():
+            ones[ctr[0] % D]()
+            ctr[0] += 1
+        el_replay = timed_region(args.steps, one, world, dist, sync)
+    if D > 1 and args.pipeline and n_pol == 1:
         batch = capture_pipeline(torch, dev, pfb, pairs, inputs, C3_N_DAT, args.steps)
         el_pipe = timed_region(1, batch, world, dist, sync)
     # kernel-event region: the K steps eagerly with HIP events around every kernel (pair 0)
@@ -655,14 +659,16 @@ def measure_c3(args, torch, dist, world, dev, pfb, lib, c3):
     kern = read_profile(lib, args.steps)
     lib.pfb_profile_reset()
     ms = el / args.steps * 1e3
-    b_alg = 16.0 * (1.0 + 8.0 / 7.0) * C3_N_DAT  # x in + chan out + chan in + output out
+    b_alg = 16.0 * (1.0 + 8.0 / 7.0) * C3_N_DAT * n_pol  # x in + chan out + chan in + output out
     gbs = b_alg / (ms * 1e-3) / 1e9
     K, n_out = pairs[0][2].shape[1], pairs[0][3].shape[1]
     res = {"workload": "C3 SKA-Mid padded round trip: 4096 ch, OS 8/7, %d two-stage firls taps, 2^26 "
-                       "samples, Nf 512, Ov 128, tukey, deripple; 1 single-pol unit per step" % len(taps),
-           "ms": round(ms, 4), "value": round(C3_N_DAT / (ms * 1e-3) / 1e6, 2),
+                       "samples, Nf 512, Ov 128, tukey, deripple; 1 %s unit per step"
+                       % (len(taps), "single-pol" if n_pol == 1 else "%d-pol" % n_pol),
+           "n_pol": n_pol,
+           "ms": round(ms, 4), "value": round(n_pol * C3_N_DAT / (ms * 1e-3) / 1e6, 2),
            "unit": "complex Msamples/s", "steps": args.steps,
-           "ms_per_replay": round(el_replay / args.steps * 1e3, 4),
+           "ms_per_replay": round(el_replay / args.steps * 1e3, 4) if el_replay else None,
            "ms_pipelined": round(el_pipe / args.steps * 1e3, 4) if el_pipe else None,
            "plan_pairs": D, "pipeline": False, "hip_graph": "one graph of the K steps on one stream",
            "unit_seeds": [300 + 7919 * p for p in range(D)],
@@ -874,6 +880,9 @@ def run_device(args, torch, dist, world, rank, local, n_pol, n_dat, seeds, c3=No
         torch.cuda.synchronize(dev)
         torch.cuda.empty_cache()
         c3_res = measure_c3(args, torch, dist, world, dev, pfb, lib, c3)
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        c3_res["dual_pol"] = measure_c3(args, torch, dist, world, dev, pfb, lib, c3, n_pol=2)
         if "cpu_baseline" in c3:
             c3_res["cpu_baseline"] = c3["cpu_baseline"]
     return {"el": el, "el_prof": el_prof, "el_serial": el_serial, "kern": kern, "copy_gbs": copy_gbs,
@@ -961,10 +970,12 @@ def report(args, res, world, workload, n_pol, n_dat, all_seeds):
         if sec is None:
             continue
         wl = f"synthesis_only_p{n_pol}" if key == "synthesis_only" else key
-        for kc in sec.get("kernels", {}).values():
-            with_traffic(kc, wl)
-            if kc["avg_ms"] > 0:
-                kc["achieved_GBs"] = round(kc["alg_bytes_per_launch"] / (kc["avg_ms"] * 1e-3) / 1e9, 1)
+        subs = [(sec, wl)] + ([(sec["dual_pol"], "c3_p2")] if key == "c3" and sec.get("dual_pol") else [])
+        for ss, w in subs:
+            for kc in ss.get("kernels", {}).values():
+                with_traffic(kc, w)
+                if kc["avg_ms"] > 0:
+                    kc["achieved_GBs"] = round(kc["alg_bytes_per_launch"] / (kc["avg_ms"] * 1e-3) / 1e9, 1)
         out[key] = sec
     out["pfb_env"] = pfb_env()
     if args.stub_device:

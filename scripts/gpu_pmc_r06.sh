@@ -8,7 +8,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $ROOT/gpurun_out
 export TMPDIR=/tmp
 cd /tmp
-declare -A KEY=([c2]=c2 [c4]=c4 [c2syn]=synthesis_only_p1 [c4syn]=synthesis_only_p2 [c3]=c3)
+declare -A KEY=([c2]=c2 [c4]=c4 [c2syn]=synthesis_only_p1 [c4syn]=synthesis_only_p2 [c3]=c3 [c3p2]=c3_p2)
 SETS=("FETCH_SIZE" "WRITE_SIZE")
 if [ -n "${SQ:-}" ]; then
   SETS+=("SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
