@@ -117,7 +117,9 @@ pfb_status pfb_analysis_execute(pfb_analysis_plan* plan, const pfb_cf32* in,
 /* Stateful stream — replaces FilterBank.execute (FilterBank.m:65-128): prepends the
  * carried-over input, runs the analysis, trims the output to a multiple of nu and
  * keeps input[T_out*M:] for the next call.  Input rounding hooks (rndInput etc.) are
- * applied by the host mirror before this call. */
+ * applied by the host mirror before this call.  Padded variant, device output: when
+ * out_capacity covers all K computed rows (not just the *n_out = T_out kept ones), rows
+ * [T_out, K) of each pol are used as scratch (the circular shift spans all K rows). */
 pfb_status pfb_filterbank_execute(pfb_analysis_plan* plan, const pfb_cf32* in,
                                   int64_t in_pol_stride, int64_t n_in, pfb_cf32* out,
                                   int64_t out_pol_stride, int64_t out_capacity,

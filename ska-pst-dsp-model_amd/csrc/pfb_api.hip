@@ -746,7 +746,11 @@ static pfb_status filterbank_exec(pfb_analysis_plan* p, const pfb_cf32* in, int6
     } else {
       dst = (float2*)out;
       dps = out_ps;
-      if (Krun != Kt) {  // padded: K rows computed; stage when the caller sized for Kt only
+      // padded: K rows computed (the circular shift spans all of them), Kt returned; they go
+      // straight into the caller's buffer when it has room for K rows (rows [Kt, K) are then
+      // scratch, pfb_filterbank_execute's contract), else through a staging buffer and a copy
+      // (round 6: the SKA-Mid cascade's stage 2 lost a 244-us copy per call)
+      if (Krun > cap) {
         HIPCHK(p->stage_out.ensure((size_t)p->n_pol * Krun * p->C * sizeof(float2)));
         dst = p->stage_out.as<float2>();
         dps = Krun * p->C;
