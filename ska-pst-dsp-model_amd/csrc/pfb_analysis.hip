@@ -31,14 +31,18 @@ struct AnaShape {
 
 // Stage x[base, base + S) into LDS (zero outside [0, n_dat)).  Interior tiles issue
 // all of their 16-byte loads back to back before the first LDS write.
+// pad > 0 (round 6, a padded stream object's carry): series sample g is pre[g] for
+// g < pad and x[g - pad] above — the concatenation of FilterBank.m:85-88 without copying it.
 template <int CH>
 __device__ __forceinline__ void stage_span(float2* smem, const float2* __restrict__ x,
-                                           int64_t base, int S, int64_t n_dat, int tid) {
+                                           int64_t base, int S, int64_t n_dat, int tid,
+                                           const float2* __restrict__ pre = nullptr, int64_t pad = 0) {
   const int S2 = (S + 1) >> 1;
-  const bool interior = base >= 0 && base + 2 * (int64_t)S2 <= n_dat &&
-                        ((reinterpret_cast<uintptr_t>(x + base) & 15) == 0);
+  const int64_t bx = base - pad;  // the span's first sample in x
+  const bool interior = bx >= 0 && bx + 2 * (int64_t)S2 <= n_dat &&
+                        ((reinterpret_cast<uintptr_t>(x + bx) & 15) == 0);
   if (interior) {
-    const float4* __restrict__ src = reinterpret_cast<const float4*>(x + base);
+    const float4* __restrict__ src = reinterpret_cast<const float4*>(x + bx);
     float4 v[CH];
 #pragma unroll
     for (int i = 0; i < CH; ++i) v[i] = src[min(tid + i * NT, S2 - 1)];
@@ -49,7 +53,13 @@ __device__ __forceinline__ void stage_span(float2* smem, const float2* __restric
   } else {
     for (int s = tid; s < S; s += NT) {
       const int64_t g = base + s;
-      smem[s] = (g >= 0 && g < n_dat) ? x[g] : make_float2(0.f, 0.f);
+      float2 v = make_float2(0.f, 0.f);
+      if (g >= pad) {
+        if (g - pad < n_dat) v = x[g - pad];
+      } else if (pre != nullptr && g >= 0) {
+        v = pre[g];
+      }
+      smem[s] = v;
     }
   }
 }
@@ -79,7 +89,7 @@ __global__ __launch_bounds__(NT) void analysis_fused_kernel(AnalysisArgs a) {
   // 2. stage the input span of the T rows (Bunton: x[k0 M + s]; padded: x[k0 M - PN + s],
   //    zero history before t = 0, polyphase_analysis_padded.m:101-102)
   const int64_t base = (VARIANT == kBunton) ? k0 * M : k0 * M - PN;
-  stage_span<S_::CH>(smem, x, base, S, a.n_dat, tid);
+  stage_span<S_::CH>(smem, x, base, S, a.n_dat, tid, a.pre ? a.pre + pol * a.pre_pol_stride : nullptr, a.pad);
   __syncthreads();
 
   // 3. FIR: Bunton u_k[n] = sum_m f[mN+n] x[kM + mN + n]        (polyphase_analysis.m:105-115)
@@ -784,13 +794,24 @@ bool analysis_can_emit_zblk(const AnalysisArgs& a) {
   return stream_shape(a) && knob("PFB_ANALYSIS_NO_STREAM") == nullptr && StreamShape<256, 13, 8, 7>::T == 16;
 }
 
+// the fused (one-launch FIR + FFT) kernel handles the shape: it stages its rows' input span
+// through stage_span, which reads a stream carry from `pre`
+bool analysis_fused_takes_carry(const AnalysisArgs& a) {
+  bool fused = false;
+  return analysis_supported(a.N, a.P, a.variant, &fused) && fused && !stream_shape(a) && a.variant != kLowCbf &&
+         knob("PFB_FUSED_NO_CARRY") == nullptr;
+}
+
 bool analysis_takes_offset(const AnalysisArgs& a) {
   return stream_shape(a) && knob("PFB_ANALYSIS_NO_STREAM") == nullptr;
 }
 
 hipError_t launch_analysis(const AnalysisArgs& a, hipStream_t s) {
   if (a.K <= a.row0) return hipSuccess;
-  if (a.pad != 0 && !analysis_takes_offset(a)) return hipErrorInvalidValue;
+  // (a read offset: the streaming kernel, or — with the carried samples in `pre` — the fused
+  // kernel, whose span staging reads them, analysis_fused_takes_carry)
+  if (a.pad != 0 && !analysis_takes_offset(a) && !(a.pre != nullptr && analysis_fused_takes_carry(a)))
+    return hipErrorInvalidValue;
   if (a.z && !analysis_can_emit_z(a)) return hipErrorInvalidValue;
   bool fused = false;
   if (!analysis_supported(a.N, a.P, a.variant, &fused)) return hipErrorInvalidValue;

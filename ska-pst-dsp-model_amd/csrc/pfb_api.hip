@@ -367,6 +367,16 @@ static bool analysis_offset_ok(const pfb_analysis_plan* p) {
   return pfb::analysis_takes_offset(a);
 }
 
+static bool analysis_fused_carry_ok(const pfb_analysis_plan* p) {
+  pfb::AnalysisArgs a{};
+  a.variant = p->variant;
+  a.N = p->N;
+  a.M = p->M;
+  a.P = p->P;
+  a.nu = p->nu;
+  return pfb::analysis_fused_takes_carry(a);
+}
+
 static bool analysis_emits_z(const pfb_analysis_plan* p) {
   pfb::AnalysisArgs a{};
   a.variant = p->variant;
@@ -706,6 +716,46 @@ static pfb_status filterbank_exec(pfb_analysis_plan* p, const pfb_cf32* in, int6
         HIPCHK(p->carry.ensure((size_t)p->n_pol * nb * sizeof(float2)));
         HIPCHK(copy_pols(p->carry.as<float2>(), nb, (const float2*)in + (input_idat - B), in_ps, nb, p->n_pol,
                          hipMemcpyDeviceToDevice, s));
+      }
+      p->buffered = std::max<int64_t>(nb, 0);
+      return PFB_OK;
+    }
+  }
+  {
+    // Carry without the concatenation copy (fused one-launch kernels: N <= 256 shapes the
+    // streaming kernel does not take, e.g. a padded cascade's stage 2): the kernel stages each
+    // row's input span from the carry (`pre`, the first B samples of the series) and the input
+    // in place (round 6; the SKA-Mid padded cascade copied its 613 MB of stage-2 series here).
+    const int64_t B = p->buffered;
+    const int64_t K = analysis_K(p, total);
+    const int64_t Kt = K - (K % p->nu);
+    const int64_t input_idat = (Kt * p->N * p->de) / p->nu;
+    if (mem == PFB_MEM_DEVICE && B > 0 && !lay && !p->lowcbf_pad && p->fused && analysis_fused_carry_ok(p) &&
+        input_idat >= B && Kt > 0) {
+      if (n_out) *n_out = Kt;
+      if (Kt > cap) return fail(PFB_ERR_BUFFER_TOO_SMALL, "output capacity %lld < %lld rows",
+                                (long long)cap, (long long)Kt);
+      const int64_t Krun = p->variant == pfb::kPadded ? K : Kt;
+      float2* dst = (float2*)out;
+      int64_t dps = out_ps;
+      if (Krun > cap) {
+        HIPCHK(p->stage_out.ensure((size_t)p->n_pol * Krun * p->C * sizeof(float2)));
+        dst = p->stage_out.as<float2>();
+        dps = Krun * p->C;
+      }
+      pfb_status st = analysis_run(p, (const float2*)in, in_ps, n_in, dst, dps, 0, Krun, K, s, nullptr, 0, 0, B,
+                                   nullptr, 0, p->carry.as<float2>());
+      if (st != PFB_OK) return st;
+      if (dst != (float2*)out)
+        HIPCHK(copy_pols((float2*)out, out_ps, dst, dps, Kt * p->C, p->n_pol, hipMemcpyDeviceToDevice, s));
+      // carry = series[input_idat, total): all of it in the new input; into the second carry
+      // buffer (the kernel just enqueued still reads the first), then swap
+      const int64_t nb = total - input_idat;
+      if (nb > 0) {
+        HIPCHK(p->carry_next.ensure((size_t)p->n_pol * nb * sizeof(float2)));
+        HIPCHK(copy_pols(p->carry_next.as<float2>(), nb, (const float2*)in + (input_idat - B), in_ps, nb, p->n_pol,
+                         hipMemcpyDeviceToDevice, s));
+        std::swap(p->carry, p->carry_next);
       }
       p->buffered = std::max<int64_t>(nb, 0);
       return PFB_OK;

@@ -101,6 +101,8 @@ bool analysis_can_emit_z(const AnalysisArgs& a);
 bool analysis_can_emit_zblk(const AnalysisArgs& a);
 // analysis shapes whose kernel reads with an input offset (AnalysisArgs::pad)
 bool analysis_takes_offset(const AnalysisArgs& a);
+// the fused kernel reads a stream carry through `pre` with `pad` (non-streaming shapes)
+bool analysis_fused_takes_carry(const AnalysisArgs& a);
 
 // Synthesis stage 1: per channelised time row, N-point inverse DFT across channels
 // (after the combine permutation and per-channel gain).  See DESIGN.md §synthesis.
